@@ -1,0 +1,228 @@
+/*
+ * pncx.h -- C-ABI of the MI355X-native XDR byte-swap + NC type-conversion path.
+ *
+ * This is the drop-in boundary for PnetCDF's per-element conversion layer.
+ * Every entry point below replaces one reference interface; the reference
+ * location is cited next to it (paths relative to the PnetCDF 1.15.0 tree).
+ * The exact reference-named symbols (ncmpii_in_swapn, ncmpii_putn_NC_<X>,
+ * ncmpii_getn_NC_<X>, ncmpii_need_convert, taking MPI_Datatype) are exported
+ * by the MPI-typed shim declared in include/pncx_ncmpii.h, which forwards to
+ * the functions here.
+ *
+ * Plain C: no HIP, torch or MPI types appear in any signature.  Buffers are
+ * plain pointers, element counts are 64-bit (MPI_Offset), streams are opaque
+ * (a hipStream_t passed as void*).  Host-buffer entry points stage through
+ * HBM and run the HIP kernels; there is no CPU conversion path.
+ */
+#ifndef PNCX_H
+#define PNCX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* NetCDF external types (src/include/pnetcdf.h.in:66-83)                    */
+/* ------------------------------------------------------------------------ */
+#ifndef NC_BYTE
+#define NC_NAT     0
+#define NC_BYTE    1
+#define NC_CHAR    2
+#define NC_SHORT   3
+#define NC_INT     4
+#define NC_FLOAT   5
+#define NC_DOUBLE  6
+#define NC_UBYTE   7
+#define NC_USHORT  8
+#define NC_UINT    9
+#define NC_INT64  10
+#define NC_UINT64 11
+#endif
+
+/* Status codes (src/include/pnetcdf.h.in:400,442,461,479) */
+#ifndef NC_NOERR
+#define NC_NOERR      0
+#define NC_EINVAL   (-36)
+#define NC_EBADTYPE (-45)
+#define NC_ECHAR    (-56)
+#define NC_ERANGE   (-60)
+#define NC_ENOMEM   (-61)
+#endif
+/* pncx-specific: a HIP runtime call failed (no device, launch error, ...) */
+#define PNCX_EDEVICE (-1900)
+
+/* CDF format numbers (src/include/pnetcdf.h.in:214-227) */
+#ifndef NC_FORMAT_CLASSIC
+#define NC_FORMAT_CLASSIC      1
+#define NC_FORMAT_64BIT_OFFSET 2
+#define NC_FORMAT_64BIT_DATA   5
+#endif
+#define PNCX_FORMAT_CDF1 1
+#define PNCX_FORMAT_CDF2 2
+#define PNCX_FORMAT_CDF5 5
+
+/* Default fill values (src/include/pnetcdf.h.in:104-114) */
+#define PNCX_FILL_BYTE   ((signed char)-127)
+#define PNCX_FILL_CHAR   ((char)0)
+#define PNCX_FILL_SHORT  ((short)-32767)
+#define PNCX_FILL_INT    (-2147483647)
+#define PNCX_FILL_FLOAT  (9.9692099683868690e+36f)
+#define PNCX_FILL_DOUBLE (9.9692099683868690e+36)
+#define PNCX_FILL_UBYTE  (255)
+#define PNCX_FILL_USHORT (65535)
+#define PNCX_FILL_UINT   (4294967295U)
+#define PNCX_FILL_INT64  ((long long)-9223372036854775806LL)
+#define PNCX_FILL_UINT64 ((unsigned long long)18446744073709551614ULL)
+
+/* MPI_Offset equivalent (64-bit signed) */
+typedef long long pncx_offset;
+
+/*
+ * Internal (in-memory) element types: one per MPI datatype accepted by the
+ * itype switch of ncmpii_putn_NC_<X>/ncmpii_getn_NC_<X>
+ * (src/drivers/common/convert_swap.m4:218-245, 285-311).  LONG is the LP64
+ * 8-byte long: same bits as LONGLONG but it keeps its own get-side fill value
+ * (NC_FILL_INT, ncx.m4:104).
+ */
+enum pncx_itype {
+    PNCX_ITYPE_SCHAR     = 1,   /* MPI_SIGNED_CHAR        */
+    PNCX_ITYPE_UCHAR     = 2,   /* MPI_UNSIGNED_CHAR      */
+    PNCX_ITYPE_SHORT     = 3,   /* MPI_SHORT              */
+    PNCX_ITYPE_USHORT    = 4,   /* MPI_UNSIGNED_SHORT     */
+    PNCX_ITYPE_INT       = 5,   /* MPI_INT                */
+    PNCX_ITYPE_UINT      = 6,   /* MPI_UNSIGNED           */
+    PNCX_ITYPE_LONG      = 7,   /* MPI_LONG (LP64)        */
+    PNCX_ITYPE_FLOAT     = 8,   /* MPI_FLOAT              */
+    PNCX_ITYPE_DOUBLE    = 9,   /* MPI_DOUBLE             */
+    PNCX_ITYPE_LONGLONG  = 10,  /* MPI_LONG_LONG_INT      */
+    PNCX_ITYPE_ULONGLONG = 11,  /* MPI_UNSIGNED_LONG_LONG */
+    PNCX_ITYPE_CHAR      = 12   /* MPI_CHAR (text only)   */
+};
+
+/* Direction of a conversion segment. */
+enum pncx_dir {
+    PNCX_PUT = 1,   /* internal (user) -> external (XDR big-endian), putn */
+    PNCX_GET = 2    /* external -> internal, getn */
+};
+
+/* Opaque stream handle: a hipStream_t (NULL = the null stream). */
+typedef void *pncx_stream_t;
+
+/* ------------------------------------------------------------------------ */
+/* Type metadata                                                             */
+/* ------------------------------------------------------------------------ */
+
+/* ncmpii_xlen_nc_type (src/drivers/common/utils.c:46-62): external size,
+ * or -1 for an unknown type. */
+int pncx_xlen(int xtype);
+/* sizeof the internal type (LP64), or -1 for an unknown itype. */
+int pncx_ilen(int itype);
+
+/* ncmpii_need_convert (src/drivers/common/convert_swap.m4:85-116):
+ * 1 if a type cast is needed between xtype and itype in CDF format
+ * `format` (1, 2 or 5), 0 if only a byte swap (or nothing) is needed. */
+int pncx_need_convert(int format, int xtype, int itype);
+
+/* NEED_BYTE_SWAP (src/drivers/include/common.h:47-54): 0 for the three
+ * 1-byte same-type pairs, 1 otherwise (little-endian host). */
+int pncx_need_swap(int xtype, int itype);
+
+/* ------------------------------------------------------------------------ */
+/* Host-buffer entry points (drop-in semantics)                              */
+/*   Buffers are caller-owned host memory, any alignment.  Data is staged    */
+/*   through HBM and converted by the HIP kernels.                           */
+/* ------------------------------------------------------------------------ */
+
+/* ncmpii_in_swapn (convert_swap.m4:137-197; proto common.h:150-151):
+ * in-place byte reversal of nelems elements of esize bytes.  No-op when
+ * esize <= 1 or nelems <= 0.  Returns NC_NOERR or PNCX_EDEVICE. */
+int pncx_in_swapn(void *buf, pncx_offset nelems, int esize);
+
+/* ncmpii_putn_NC_<X> (convert_swap.m4:202-264; proto common.h:153-186):
+ * convert nelems elements of itype from ibuf into external type xtype at
+ * xbuf (big-endian).  cdf_ver matters only for xtype NC_BYTE (CDF-1/2 treat
+ * NC_BYTE<-uchar as a raw copy, convert_swap.m4:219-222).  fillp points to
+ * the fill value of xtype in native byte order (ncmpio_util.c:705-711), or
+ * NULL (then the reference's NULL-fill behaviour is reproduced).
+ * Returns NC_NOERR, NC_ERANGE (non-fatal; all elements are converted,
+ * out-of-range ones are filled, ncx.m4:2693-2698), NC_EBADTYPE,
+ * NC_ECHAR or PNCX_EDEVICE. */
+int pncx_putn(int cdf_ver, int xtype, void *xbuf, const void *ibuf,
+              pncx_offset nelems, int itype, const void *fillp);
+
+/* ncmpii_getn_NC_<X> (convert_swap.m4:270-330; proto common.h:188-221):
+ * convert nelems external elements at xbuf into itype at ibuf.  Out-of-range
+ * elements receive the default fill value of itype (ncx.m4:97-111) and the
+ * call returns NC_ERANGE. */
+int pncx_getn(int cdf_ver, int xtype, const void *xbuf, void *ibuf,
+              pncx_offset nelems, int itype);
+
+/* ------------------------------------------------------------------------ */
+/* Device-resident entry points (new API: the reference has no device side) */
+/*   All pointers are device (HBM) pointers except fillp (host).  Calls are  */
+/*   asynchronous on `stream` and capture-safe (no allocation, no sync).     */
+/*   dstatus: device int; the kernels store NC_ERANGE into it when any       */
+/*   element is out of range and never clear it (may be NULL).               */
+/* ------------------------------------------------------------------------ */
+
+/* In-place swap of an HBM slab (the config-2 / config-5 hot kernel). */
+int pncx_dev_in_swapn(void *dbuf, pncx_offset nelems, int esize,
+                      pncx_stream_t stream);
+
+/* Out-of-place swap, dst may equal src (ncx.m4:297-467 swapn2b/4b/8b). */
+int pncx_dev_swapn(void *ddst, const void *dsrc, pncx_offset nelems,
+                   int esize, pncx_stream_t stream);
+
+int pncx_dev_putn(int cdf_ver, int xtype, void *dxbuf, const void *dibuf,
+                  pncx_offset nelems, int itype, const void *fillp,
+                  int *dstatus, pncx_stream_t stream);
+
+int pncx_dev_getn(int cdf_ver, int xtype, const void *dxbuf, void *dibuf,
+                  pncx_offset nelems, int itype, int *dstatus,
+                  pncx_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Batched conversion: many independent requests in one launch per         */
+/* conversion class (replaces the per-request loop of                       */
+/* ncmpio_igetput_varm, ncmpio_i_getput.m4:300-303, and the per-request      */
+/* unpack at wait time, ncmpio_wait.c:743-781).                              */
+/* ------------------------------------------------------------------------ */
+typedef struct pncx_seg {
+    int          dir;       /* PNCX_PUT or PNCX_GET                          */
+    int          cdf_ver;   /* 1, 2 or 5                                     */
+    int          xtype;     /* NC_BYTE .. NC_UINT64                          */
+    int          itype;     /* enum pncx_itype                               */
+    pncx_offset  nelems;
+    void        *xbuf;      /* external buffer                               */
+    void        *ibuf;      /* internal buffer; may equal xbuf for same-type */
+    const void  *fillp;     /* PUT only: xtype fill value (native) or NULL   */
+} pncx_seg;
+
+/* Device buffers.  status_out[i] (host array, may be NULL) receives the
+ * status of segment i after the call completes (this call synchronises the
+ * stream).  Returns the first non-NOERR segment status. */
+int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out,
+                   pncx_stream_t stream);
+
+/* Host buffers (staged through HBM). */
+int pncx_batch(const pncx_seg *segs, int nseg, int *status_out);
+
+/* ------------------------------------------------------------------------ */
+/* Runtime helpers                                                           */
+/* ------------------------------------------------------------------------ */
+int  pncx_device_count(void);
+int  pncx_set_device(int dev);
+int  pncx_get_device(void);
+/* Synchronise `stream` and return *dstatus (NC_NOERR if it was 0). */
+int  pncx_dev_status_read(const int *dstatus, pncx_stream_t stream);
+const char *pncx_strerror(int err);
+/* Version string of the library build (arch, kernel set). */
+const char *pncx_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PNCX_H */

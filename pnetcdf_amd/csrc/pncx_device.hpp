@@ -1,0 +1,264 @@
+// pncx_device.hpp -- device-side element semantics of the XDR swap / NC type
+// conversion path, written for gfx950 (CDNA4).
+//
+// One function per direction (get1: external -> internal, put1: internal ->
+// external), specialised at compile time on (xtype, itype).  The rules are
+// those of PnetCDF's ncx.m4 with ERANGE_FILL (see the oracle for the
+// per-macro citations); the float->int casts reproduce what the reference's
+// x86-64 gcc -O2 build does for NaN and for the 2^63 / 2^64 edges, because
+// the GPU conversion instructions differ there (v_cvt_i32_f64(NaN) = 0).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+
+#include "../../include/pncx.h"
+
+namespace pncx {
+
+// ---------------------------------------------------------------------------
+// external types (pnetcdf.h.in:66-83) and their limits (ncx_h.m4:81-106)
+// ---------------------------------------------------------------------------
+template <int XT> struct X;
+#define PNCX_XDEF(XT_, CT_, UT_, FLT_, LO_, HI_, FILL_)                     \
+    template <> struct X<XT_> {                                           \
+        using T = CT_;                                                    \
+        using U = UT_;                                                    \
+        static constexpr int size = sizeof(CT_);                          \
+        static constexpr bool is_float = FLT_;                            \
+        static constexpr long long lo = LO_;                              \
+        static constexpr unsigned long long hi = HI_;                     \
+        __device__ static constexpr T fill() { return (T)(FILL_); }       \
+    };
+PNCX_XDEF(NC_BYTE,   int8_t,   uint8_t,  false, -128, 127ull, -127)
+PNCX_XDEF(NC_UBYTE,  uint8_t,  uint8_t,  false, 0, 255ull, 255)
+PNCX_XDEF(NC_SHORT,  int16_t,  uint16_t, false, -32768, 32767ull, -32767)
+PNCX_XDEF(NC_USHORT, uint16_t, uint16_t, false, 0, 65535ull, 65535)
+PNCX_XDEF(NC_INT,    int32_t,  uint32_t, false, -2147483647LL - 1, 2147483647ull, -2147483647)
+PNCX_XDEF(NC_UINT,   uint32_t, uint32_t, false, 0, 4294967295ull, 4294967295u)
+PNCX_XDEF(NC_FLOAT,  float,    uint32_t, true, 0, 0, 9.9692099683868690e+36f)
+PNCX_XDEF(NC_DOUBLE, double,   uint64_t, true, 0, 0, 9.9692099683868690e+36)
+PNCX_XDEF(NC_INT64,  int64_t,  uint64_t, false, -9223372036854775807LL - 1, 9223372036854775807ull,
+          -9223372036854775806LL)
+PNCX_XDEF(NC_UINT64, uint64_t, uint64_t, false, 0, 18446744073709551615ull, 18446744073709551614ull)
+#undef PNCX_XDEF
+
+// ---------------------------------------------------------------------------
+// internal types (convert_swap.m4:218-245) with their get-side default fill
+// (FillDefaultValue, ncx.m4:97-111: long -> NC_FILL_INT)
+// ---------------------------------------------------------------------------
+template <int IT> struct I;
+#define PNCX_IDEF(IT_, CT_, UT_, FLT_, LO_, HI_, FILL_)                     \
+    template <> struct I<IT_> {                                           \
+        using T = CT_;                                                    \
+        using U = UT_;                                                    \
+        static constexpr int size = sizeof(CT_);                          \
+        static constexpr bool is_float = FLT_;                            \
+        static constexpr long long lo = LO_;                              \
+        static constexpr unsigned long long hi = HI_;                     \
+        __device__ static constexpr T fill() { return (T)(FILL_); }       \
+    };
+PNCX_IDEF(PNCX_ITYPE_SCHAR,     int8_t,   uint8_t,  false, -128, 127ull, -127)
+PNCX_IDEF(PNCX_ITYPE_UCHAR,     uint8_t,  uint8_t,  false, 0, 255ull, 255)
+PNCX_IDEF(PNCX_ITYPE_SHORT,     int16_t,  uint16_t, false, -32768, 32767ull, -32767)
+PNCX_IDEF(PNCX_ITYPE_USHORT,    uint16_t, uint16_t, false, 0, 65535ull, 65535)
+PNCX_IDEF(PNCX_ITYPE_INT,       int32_t,  uint32_t, false, -2147483647LL - 1, 2147483647ull, -2147483647)
+PNCX_IDEF(PNCX_ITYPE_UINT,      uint32_t, uint32_t, false, 0, 4294967295ull, 4294967295u)
+PNCX_IDEF(PNCX_ITYPE_LONG,      int64_t,  uint64_t, false, -9223372036854775807LL - 1,
+          9223372036854775807ull, -2147483647)
+PNCX_IDEF(PNCX_ITYPE_FLOAT,     float,    uint32_t, true, 0, 0, 9.9692099683868690e+36f)
+PNCX_IDEF(PNCX_ITYPE_DOUBLE,    double,   uint64_t, true, 0, 0, 9.9692099683868690e+36)
+PNCX_IDEF(PNCX_ITYPE_LONGLONG,  int64_t,  uint64_t, false, -9223372036854775807LL - 1,
+          9223372036854775807ull, -9223372036854775806LL)
+PNCX_IDEF(PNCX_ITYPE_ULONGLONG, uint64_t, uint64_t, false, 0, 18446744073709551615ull,
+          18446744073709551614ull)
+#undef PNCX_IDEF
+
+// ---------------------------------------------------------------------------
+// byte order: the XDR external form is big-endian (SWAP2/4/8, ncx.m4:279-294)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint8_t bswap(uint8_t v) { return v; }
+__device__ __forceinline__ uint16_t bswap(uint16_t v) { return __builtin_bswap16(v); }
+__device__ __forceinline__ uint32_t bswap(uint32_t v) { return __builtin_bswap32(v); }
+__device__ __forceinline__ uint64_t bswap(uint64_t v) { return __builtin_bswap64(v); }
+
+template <typename T, typename U>
+__device__ __forceinline__ T bits_to(U u) {
+    static_assert(sizeof(T) == sizeof(U), "size");
+    T t;
+    __builtin_memcpy(&t, &u, sizeof t);
+    return t;
+}
+
+// ---------------------------------------------------------------------------
+// x86-64 gcc cast emulation.  cvttsd2si returns the
+// "integer indefinite" value 0x80..0 for NaN and out-of-range inputs; narrow
+// targets are converted through 32 bits, uint32 through 64 bits, and uint64
+// through gcc's compare-with-2^63 sequence.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int32_t cvtt_i32(double x) {
+    return (x >= -2147483648.0 && x < 2147483648.0) ? (int32_t)x : INT32_MIN;
+}
+__device__ __forceinline__ int64_t cvtt_i64(double x) {
+    return (x >= -9223372036854775808.0 && x < 9223372036854775808.0) ? (int64_t)x : INT64_MIN;
+}
+__device__ __forceinline__ uint64_t cvtt_u64(double x) {
+    if (x >= 9223372036854775808.0)   // comisd 2^63; jnb (false for NaN)
+        return (uint64_t)cvtt_i64(x - 9223372036854775808.0) ^ 0x8000000000000000ull;
+    return (uint64_t)cvtt_i64(x);
+}
+// C cast (T)x of a floating value as compiled by gcc -O2 on x86-64
+template <typename T>
+__device__ __forceinline__ T x86_cast(double x) {
+    if constexpr (std::is_same<T, int8_t>::value || std::is_same<T, uint8_t>::value ||
+                  std::is_same<T, int16_t>::value || std::is_same<T, uint16_t>::value ||
+                  std::is_same<T, int32_t>::value)
+        return (T)cvtt_i32(x);
+    else if constexpr (std::is_same<T, uint32_t>::value)
+        return (T)cvtt_i64(x);
+    else if constexpr (std::is_same<T, int64_t>::value)
+        return cvtt_i64(x);
+    else
+        return cvtt_u64(x);
+}
+
+// cvtsd2ss / cvtss2sd: RNE value conversion; NaN keeps sign and the top
+// payload bits and is quieted.
+__device__ __forceinline__ float f64_to_f32(double x) {
+    uint64_t b = bits_to<uint64_t>(x);
+    if ((b & 0x7fffffffffffffffull) > 0x7ff0000000000000ull) {
+        uint32_t r = ((uint32_t)(b >> 32) & 0x80000000u) | 0x7fc00000u |
+                     (uint32_t)((b >> 29) & 0x3fffffu);
+        return bits_to<float>(r);
+    }
+    return (float)x;
+}
+__device__ __forceinline__ double f32_to_f64(float x) {
+    uint32_t b = bits_to<uint32_t>(x);
+    if ((b & 0x7fffffffu) > 0x7f800000u) {
+        uint64_t r = ((uint64_t)(b & 0x80000000u) << 32) | 0x7ff8000000000000ull |
+                     ((uint64_t)(b & 0x3fffffu) << 29);
+        return bits_to<double>(r);
+    }
+    return (double)x;
+}
+
+// exact integer range test (NCX_GET1I / NCX_PUT1I checks are exact)
+template <typename S>
+__device__ __forceinline__ bool in_range(S v, long long lo, unsigned long long hi) {
+    if constexpr (std::is_signed<S>::value) {
+        long long x = (long long)v;
+        if (x < lo) return false;
+        if (x < 0) return true;
+        return (unsigned long long)x <= hi;
+    } else {
+        return (unsigned long long)v <= hi;
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ double as_double(T v) {
+    if constexpr (std::is_same<T, float>::value) return f32_to_f64(v);
+    else return (double)v;
+}
+
+// ---------------------------------------------------------------------------
+// GET: one external value (already byte-swapped to native) -> internal value
+// ---------------------------------------------------------------------------
+template <int XT, int IT>
+__device__ __forceinline__ typename I<IT>::T get1(typename X<XT>::T xx, bool &bad) {
+    using XI = X<XT>;
+    using II = I<IT>;
+    using IT_T = typename II::T;
+    if constexpr (!XI::is_float && !II::is_float) {
+        // NCX_GET1I (ncx.m4:560-598), NCX_GETN_BYTE (:2369-2392),
+        // uchar->schar (:2817-2834): exact range test, fill = default of itype
+        if (in_range(xx, II::lo, II::hi)) return (IT_T)xx;
+        bad = true;
+        return II::fill();
+    } else if constexpr (!XI::is_float && II::is_float) {
+        return (IT_T)xx;                        // int -> float/double (ncx.m4:551)
+    } else if constexpr (XI::is_float && II::is_float) {
+        if constexpr (XT == NC_FLOAT) {
+            return f32_to_f64(xx);              // float -> double, exact (:546)
+        } else {                                // get_NC_DOUBLE_float (:1834-1849)
+            if (xx > 3.40282346638528859811704183484516925e+38 ||
+                xx < -3.40282346638528859811704183484516925e+38) {
+                bad = true;
+                return II::fill();
+            }
+            return f64_to_f32(xx);
+        }
+    } else {
+        const double d = as_double(xx);
+        if constexpr (IT == PNCX_ITYPE_LONGLONG) {             // GETF_CheckBND2 (:518-527)
+            if (d == 9223372036854775808.0) return INT64_MAX;
+            if (d == -9223372036854775808.0) return INT64_MIN;
+            if (d > 9223372036854775808.0 || d < -9223372036854775808.0) { bad = true; return II::fill(); }
+            return cvtt_i64(d);
+        } else if constexpr (IT == PNCX_ITYPE_ULONGLONG) {
+            if (d == 18446744073709551616.0) return UINT64_MAX;
+            if (d > 18446744073709551616.0 || d < 0.0) { bad = true; return II::fill(); }
+            return cvtt_u64(d);
+        } else if constexpr (IT == PNCX_ITYPE_LONG) {          // GETF_CheckBND + :511
+            if (d > 9223372036854775808.0 || d < -9223372036854775808.0) { bad = true; return II::fill(); }
+            if (d == 9223372036854775808.0) return INT64_MAX;
+            return cvtt_i64(d);
+        } else {                                               // GETF_CheckBND (:503-513)
+            const double hi = (double)II::hi;
+            const double lo = (double)II::lo;
+            if (d > hi || d < lo) { bad = true; return II::fill(); }
+            return x86_cast<IT_T>(d);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// PUT: one internal value -> external value (native order; caller swaps)
+//   fill: value written for out-of-range elements (the variable's fill value,
+//   or the xtype default when fillp == NULL, NCX_PUT1I/PUT1F ncx.m4:610,642)
+// ---------------------------------------------------------------------------
+template <int XT, int IT>
+__device__ __forceinline__ typename X<XT>::T put1(typename I<IT>::T v, typename X<XT>::T fill,
+                                                  bool &bad) {
+    using XI = X<XT>;
+    using II = I<IT>;
+    using XT_T = typename XI::T;
+    if constexpr (!XI::is_float && !II::is_float) {
+        // NCX_PUT1I (:631-665), NCX_PUTN_BYTE (:2561-2581) and the
+        // hand-written <- schar/uchar codecs: exact range test
+        if (in_range(v, XI::lo, XI::hi)) return (XT_T)v;
+        bad = true;
+        return fill;
+    } else if constexpr (!XI::is_float && II::is_float) {
+        // NCX_PUT1F (:604-625) / NCX_PUTN_BYTE with a float itype
+        const double d = as_double(v);
+        const double hi = (double)XI::hi;     // 2^63 / 2^64 for the 64-bit ones
+        const double lo = (double)XI::lo;
+        if (d > hi || d < lo) { bad = true; return fill; }
+        return x86_cast<XT_T>(d);
+    } else if constexpr (XI::is_float && !II::is_float) {
+        return (XT_T)v;                        // integer -> float/double, RNE
+    } else if constexpr (XT == NC_FLOAT) {     // NCX_PUT1F(float, double) (:612)
+        if (v > 3.40282346638528859811704183484516925e+38 ||
+            v < -3.40282346638528859811704183484516925e+38) { bad = true; return fill; }
+        return f64_to_f32(v);
+    } else {                                   // put_NC_DOUBLE_float (:1871-1886)
+        const double d = f32_to_f64(v);
+        if (d > 1.7976931348623157e+308 || d < -1.7976931348623157e+308) { bad = true; return fill; }
+        return d;
+    }
+}
+
+// pairs whose reference codec writes nothing (1-byte externals) or swaps the
+// bytes already in xbuf (ushort/uint <- schar, ncx.m4:818-841, 1036-1056)
+// when fillp == NULL
+template <int XT, int IT>
+struct null_fill_preserves {
+    static constexpr bool value =
+        (XT == NC_BYTE || XT == NC_UBYTE) ||
+        ((XT == NC_USHORT || XT == NC_UINT) && IT == PNCX_ITYPE_SCHAR);
+};
+
+}  // namespace pncx

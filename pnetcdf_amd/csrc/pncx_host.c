@@ -1,0 +1,635 @@
+/*
+ * pncx_host.c -- C host side of libpncx: the include/pncx.h entry points.
+ *
+ * Classifies each request the way the reference's convert_swap.m4 /
+ * ncmpio_util.c buffer policy does (copy, byte swap, or cast+swap), builds
+ * the launch descriptors, and for host buffers stages the data through HBM
+ * in chunks on two HIP streams so the copies of one chunk overlap the
+ * kernel of the other.  All device work goes through the thin C-ABI shim
+ * (pncx_shim.h); there is no CPU conversion code in this library.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/pncx.h"
+#include "pncx_shim.h"
+
+/* ------------------------------------------------------------------------ */
+/* type metadata                                                             */
+/* ------------------------------------------------------------------------ */
+int pncx_xlen(int xtype)                     /* ncmpii_xlen_nc_type, utils.c:46-62 */
+{
+    switch (xtype) {
+        case NC_BYTE: case NC_UBYTE: case NC_CHAR: return 1;
+        case NC_SHORT: case NC_USHORT: return 2;
+        case NC_INT: case NC_UINT: case NC_FLOAT: return 4;
+        case NC_DOUBLE: case NC_INT64: case NC_UINT64: return 8;
+        default: return -1;
+    }
+}
+
+int pncx_ilen(int itype)
+{
+    switch (itype) {
+        case PNCX_ITYPE_SCHAR: case PNCX_ITYPE_UCHAR: case PNCX_ITYPE_CHAR: return 1;
+        case PNCX_ITYPE_SHORT: case PNCX_ITYPE_USHORT: return 2;
+        case PNCX_ITYPE_INT: case PNCX_ITYPE_UINT: case PNCX_ITYPE_FLOAT: return 4;
+        case PNCX_ITYPE_LONG: case PNCX_ITYPE_DOUBLE: case PNCX_ITYPE_LONGLONG:
+        case PNCX_ITYPE_ULONGLONG: return 8;
+        default: return -1;
+    }
+}
+
+int pncx_need_convert(int format, int xtype, int itype)  /* convert_swap.m4:85-116 */
+{
+    if (xtype == NC_CHAR) return 0;
+    if (format < PNCX_FORMAT_CDF5 && xtype == NC_BYTE && itype == PNCX_ITYPE_UCHAR) return 0;
+    if (itype == PNCX_ITYPE_LONG) itype = PNCX_ITYPE_LONGLONG;
+    return !((xtype == NC_BYTE   && itype == PNCX_ITYPE_SCHAR)    ||
+             (xtype == NC_SHORT  && itype == PNCX_ITYPE_SHORT)    ||
+             (xtype == NC_INT    && itype == PNCX_ITYPE_INT)      ||
+             (xtype == NC_FLOAT  && itype == PNCX_ITYPE_FLOAT)    ||
+             (xtype == NC_DOUBLE && itype == PNCX_ITYPE_DOUBLE)   ||
+             (xtype == NC_UBYTE  && itype == PNCX_ITYPE_UCHAR)    ||
+             (xtype == NC_USHORT && itype == PNCX_ITYPE_USHORT)   ||
+             (xtype == NC_UINT   && itype == PNCX_ITYPE_UINT)     ||
+             (xtype == NC_INT64  && itype == PNCX_ITYPE_LONGLONG) ||
+             (xtype == NC_UINT64 && itype == PNCX_ITYPE_ULONGLONG));
+}
+
+int pncx_need_swap(int xtype, int itype)                 /* common.h:47-54 */
+{
+    return ((xtype == NC_CHAR  && itype == PNCX_ITYPE_CHAR)  ||
+            (xtype == NC_BYTE  && itype == PNCX_ITYPE_SCHAR) ||
+            (xtype == NC_UBYTE && itype == PNCX_ITYPE_UCHAR)) ? 0 : 1;
+}
+
+const char *pncx_strerror(int err)
+{
+    switch (err) {
+        case NC_NOERR: return "No error";
+        case NC_EINVAL: return "Invalid argument";
+        case NC_EBADTYPE: return "Not a netcdf data type";
+        case NC_ECHAR: return "Attempt to convert between text & numbers";
+        case NC_ERANGE: return "Numeric conversion not representable";
+        case NC_ENOMEM: return "Memory allocation (malloc) failure";
+        case PNCX_EDEVICE: {
+            const char *e = pncxrt_last_error();
+            return (e && e[0]) ? e : "HIP device error";
+        }
+        default: return "Unknown error";
+    }
+}
+
+const char *pncx_version(void) { return "pncx 0.1 gfx950 (swap 2/4/8/n, 10x11 get/put, batch)"; }
+
+int pncx_device_count(void) { return pncxrt_device_count(); }
+int pncx_set_device(int dev) { return pncxrt_set_device(dev); }
+int pncx_get_device(void) { return pncxrt_get_device(); }
+
+/* ------------------------------------------------------------------------ */
+/* classification of one request                                             */
+/* ------------------------------------------------------------------------ */
+typedef struct op_t {
+    int kind;      /* PNCXK_SWAP / PNCXK_GET / PNCXK_PUT       */
+    int a, b, c;   /* esize | xtype, itype, preserve          */
+    int ss, ds;    /* source / destination element bytes      */
+    unsigned long long fill;
+} op_t;
+
+static int null_fill_preserves(int xtype, int itype)
+{
+    return xtype == NC_BYTE || xtype == NC_UBYTE ||
+           ((xtype == NC_USHORT || xtype == NC_UINT) && itype == PNCX_ITYPE_SCHAR);
+}
+
+static unsigned long long default_fill_bits(int xtype)   /* pnetcdf.h.in:104-114 */
+{
+    unsigned long long b = 0;
+    switch (xtype) {
+        case NC_BYTE:   { signed char v = PNCX_FILL_BYTE; memcpy(&b, &v, 1); break; }
+        case NC_UBYTE:  { unsigned char v = PNCX_FILL_UBYTE; memcpy(&b, &v, 1); break; }
+        case NC_SHORT:  { short v = PNCX_FILL_SHORT; memcpy(&b, &v, 2); break; }
+        case NC_USHORT: { unsigned short v = PNCX_FILL_USHORT; memcpy(&b, &v, 2); break; }
+        case NC_INT:    { int v = PNCX_FILL_INT; memcpy(&b, &v, 4); break; }
+        case NC_UINT:   { unsigned v = PNCX_FILL_UINT; memcpy(&b, &v, 4); break; }
+        case NC_FLOAT:  { float v = PNCX_FILL_FLOAT; memcpy(&b, &v, 4); break; }
+        case NC_DOUBLE: { double v = PNCX_FILL_DOUBLE; memcpy(&b, &v, 8); break; }
+        case NC_INT64:  { long long v = PNCX_FILL_INT64; memcpy(&b, &v, 8); break; }
+        case NC_UINT64: { unsigned long long v = PNCX_FILL_UINT64; memcpy(&b, &v, 8); break; }
+        default: break;
+    }
+    return b;
+}
+
+/* dir: PNCX_PUT or PNCX_GET.  Mirrors ncmpii_{put,get}n_NC_<X> dispatch
+ * (convert_swap.m4:202-330) including the CDF-1/2 NC_BYTE<->uchar copy. */
+static int classify(int dir, int cdf_ver, int xtype, int itype, const void *fillp, op_t *op)
+{
+    const int xs = pncx_xlen(xtype), is = pncx_ilen(itype);
+    memset(op, 0, sizeof *op);
+    if (xs < 0 || is < 0) return NC_EBADTYPE;
+    if ((xtype == NC_CHAR) != (itype == PNCX_ITYPE_CHAR)) return NC_ECHAR;
+    if (dir != PNCX_PUT && dir != PNCX_GET) return NC_EINVAL;
+    op->ss = dir == PNCX_PUT ? is : xs;
+    op->ds = dir == PNCX_PUT ? xs : is;
+    if (xtype == NC_CHAR || !pncx_need_convert(cdf_ver, xtype, itype)) {
+        op->kind = PNCXK_SWAP;        /* same representation: swap (or copy) */
+        op->a = xs;
+        return NC_NOERR;
+    }
+    op->kind = dir == PNCX_PUT ? PNCXK_PUT : PNCXK_GET;
+    op->a = xtype;
+    op->b = itype;
+    if (dir == PNCX_PUT) {
+        if (fillp != NULL) memcpy(&op->fill, fillp, (size_t)xs);
+        else {
+            op->fill = default_fill_bits(xtype);
+            op->c = null_fill_preserves(xtype, itype);
+        }
+    }
+    return NC_NOERR;
+}
+
+static int launch_op(const op_t *op, const void *src, void *dst, long long n, int *dstatus,
+                     void *stream)
+{
+    pncxk_args a;
+    a.src = src;
+    a.dst = dst;
+    a.n = n;
+    a.fill = op->fill;
+    a.status = dstatus;
+    a.stream = stream;
+    a.nontemporal = 0;
+    switch (op->kind) {
+        case PNCXK_SWAP: return pncxk_swap(op->a, &a);
+        case PNCXK_GET: return pncxk_get(op->a, op->b, &a);
+        case PNCXK_PUT: return pncxk_put(op->a, op->b, op->c, &a);
+        default: return NC_EINVAL;
+    }
+}
+
+static int have_device(void) { return pncxrt_device_count() > 0; }
+
+/* ------------------------------------------------------------------------ */
+/* device-resident entry points                                              */
+/* ------------------------------------------------------------------------ */
+int pncx_dev_swapn(void *ddst, const void *dsrc, pncx_offset nelems, int esize,
+                   pncx_stream_t stream)
+{
+    pncxk_args a;
+    if (esize <= 0) return NC_EINVAL;
+    if (nelems <= 0) return NC_NOERR;
+    if (!have_device()) return PNCX_EDEVICE;
+    if (esize == 1) {
+        if (ddst == dsrc) return NC_NOERR;
+        return pncxrt_memcpy_d2d(ddst, dsrc, (size_t)nelems, stream);
+    }
+    memset(&a, 0, sizeof a);
+    a.src = dsrc;
+    a.dst = ddst;
+    a.n = nelems;
+    a.stream = stream;
+    {
+        const char *nt = getenv("PNCX_NONTEMPORAL");
+        a.nontemporal = nt ? atoi(nt) : 0;
+    }
+    return pncxk_swap(esize, &a);
+}
+
+int pncx_dev_in_swapn(void *dbuf, pncx_offset nelems, int esize, pncx_stream_t stream)
+{
+    if (esize <= 1 || nelems <= 0) return NC_NOERR;          /* convert_swap.m4:147 */
+    return pncx_dev_swapn(dbuf, dbuf, nelems, esize, stream);
+}
+
+int pncx_dev_putn(int cdf_ver, int xtype, void *dxbuf, const void *dibuf, pncx_offset nelems,
+                  int itype, const void *fillp, int *dstatus, pncx_stream_t stream)
+{
+    op_t op;
+    int err = classify(PNCX_PUT, cdf_ver, xtype, itype, fillp, &op);
+    if (err != NC_NOERR) return err;
+    if (nelems <= 0) return NC_NOERR;
+    if (!have_device()) return PNCX_EDEVICE;
+    if (op.kind == PNCXK_SWAP && op.a == 1)
+        return dxbuf == dibuf ? NC_NOERR : pncxrt_memcpy_d2d(dxbuf, dibuf, (size_t)nelems, stream);
+    return launch_op(&op, dibuf, dxbuf, nelems, dstatus, stream);
+}
+
+int pncx_dev_getn(int cdf_ver, int xtype, const void *dxbuf, void *dibuf, pncx_offset nelems,
+                  int itype, int *dstatus, pncx_stream_t stream)
+{
+    op_t op;
+    int err = classify(PNCX_GET, cdf_ver, xtype, itype, NULL, &op);
+    if (err != NC_NOERR) return err;
+    if (nelems <= 0) return NC_NOERR;
+    if (!have_device()) return PNCX_EDEVICE;
+    if (op.kind == PNCXK_SWAP && op.a == 1)
+        return dxbuf == dibuf ? NC_NOERR : pncxrt_memcpy_d2d(dibuf, dxbuf, (size_t)nelems, stream);
+    return launch_op(&op, dxbuf, dibuf, nelems, dstatus, stream);
+}
+
+int pncx_dev_status_read(const int *dstatus, pncx_stream_t stream)
+{
+    int v = 0, err;
+    if (dstatus == NULL) return NC_NOERR;
+    err = pncxrt_memcpy_d2h(&v, dstatus, sizeof v, stream);
+    if (err == 0) err = pncxrt_stream_sync(stream);
+    if (err != 0) return PNCX_EDEVICE;
+    return v;
+}
+
+/* ------------------------------------------------------------------------ */
+/* per-device staging context for host-buffer calls                          */
+/* ------------------------------------------------------------------------ */
+#define NSLOT 2
+#define MAX_DEV 64
+
+typedef struct ctx_t {
+    int    init;
+    void  *stream[NSLOT];
+    void  *dbuf[NSLOT];       /* device staging, one per slot  */
+    size_t dbuf_size;
+    int   *dstatus;           /* device status words [NSLOT]   */
+    void  *dscratch;          /* batch descriptors / statuses  */
+    size_t dscratch_size;
+    pthread_mutex_t lock;
+} ctx_t;
+
+static ctx_t g_ctx[MAX_DEV];
+static pthread_mutex_t g_ctx_lock = PTHREAD_MUTEX_INITIALIZER;
+
+static size_t chunk_bytes(void)
+{
+    static size_t v = 0;
+    if (v == 0) {
+        const char *e = getenv("PNCX_CHUNK_MB");
+        long mb = e ? atol(e) : 64;
+        if (mb <= 0) mb = 64;
+        v = (size_t)mb << 20;
+    }
+    return v;
+}
+
+static ctx_t *get_ctx(void)
+{
+    int dev = pncxrt_get_device(), i;
+    ctx_t *c;
+    if (dev < 0 || dev >= MAX_DEV) return NULL;
+    c = &g_ctx[dev];
+    pthread_mutex_lock(&g_ctx_lock);
+    if (!c->init) {
+        int err = 0;
+        memset(c, 0, sizeof *c);
+        pthread_mutex_init(&c->lock, NULL);
+        for (i = 0; i < NSLOT && !err; i++) err = pncxrt_stream_create(&c->stream[i]);
+        if (!err) err = pncxrt_malloc((void **)&c->dstatus, NSLOT * sizeof(int));
+        if (err) {
+            pthread_mutex_unlock(&g_ctx_lock);
+            return NULL;
+        }
+        c->init = 1;
+    }
+    pthread_mutex_unlock(&g_ctx_lock);
+    return c;
+}
+
+static int ensure_dbuf(ctx_t *c, size_t need)
+{
+    int i;
+    if (c->dbuf_size >= need) return 0;
+    for (i = 0; i < NSLOT; i++) {
+        if (c->stream[i]) pncxrt_stream_sync(c->stream[i]);
+        pncxrt_free(c->dbuf[i]);
+        c->dbuf[i] = NULL;
+    }
+    c->dbuf_size = 0;
+    for (i = 0; i < NSLOT; i++)
+        if (pncxrt_malloc(&c->dbuf[i], need) != 0) return PNCX_EDEVICE;
+    c->dbuf_size = need;
+    return 0;
+}
+
+static int ensure_scratch(ctx_t *c, size_t need)
+{
+    if (c->dscratch_size >= need) return 0;
+    pncxrt_stream_sync(c->stream[0]);
+    pncxrt_free(c->dscratch);
+    c->dscratch = NULL;
+    c->dscratch_size = 0;
+    if (pncxrt_malloc(&c->dscratch, need) != 0) return PNCX_EDEVICE;
+    c->dscratch_size = need;
+    return 0;
+}
+
+#define ALIGN16(x) (((x) + 15) & ~(size_t)15)
+
+/*
+ * Stage src (n elements of op->ss bytes, host) -> kernel -> dst (host).
+ * Chunks alternate between two streams/slots: while chunk k's kernel runs,
+ * chunk k-1's result streams back and chunk k+1's input streams in.
+ * preserve: the destination's current content is needed (NULL-fill codecs).
+ */
+static int host_staged(const op_t *op, const void *src, void *dst, long long n, int preserve)
+{
+    ctx_t *c = get_ctx();
+    size_t per_elem, chunk_elems, cb;
+    long long off;
+    int slot, err = 0, st0 = 0, st1 = 0, i;
+    if (c == NULL) return PNCX_EDEVICE;
+    pthread_mutex_lock(&c->lock);
+    per_elem = (size_t)op->ss + (size_t)op->ds;
+    cb = chunk_bytes();
+    chunk_elems = cb / per_elem;
+    if (chunk_elems < 1) chunk_elems = 1;
+    if ((long long)chunk_elems > n) chunk_elems = (size_t)n;
+    err = ensure_dbuf(c, ALIGN16(chunk_elems * op->ss) + ALIGN16(chunk_elems * op->ds));
+    for (i = 0; i < NSLOT && !err; i++)
+        err = pncxrt_memset(c->dstatus + i, 0, sizeof(int), c->stream[i]);
+    for (off = 0, slot = 0; off < n && !err; off += (long long)chunk_elems, slot ^= 1) {
+        long long m = n - off < (long long)chunk_elems ? n - off : (long long)chunk_elems;
+        uint8_t *din = (uint8_t *)c->dbuf[slot];
+        uint8_t *dout = din + ALIGN16(chunk_elems * op->ss);
+        void *s = c->stream[slot];
+        const uint8_t *hs = (const uint8_t *)src + (size_t)off * op->ss;
+        uint8_t *hd = (uint8_t *)dst + (size_t)off * op->ds;
+        if (op->ss == op->ds && src == dst) dout = din;      /* in-place swap */
+        err = pncxrt_memcpy_h2d(din, hs, (size_t)m * op->ss, s);
+        if (!err && preserve && dout != din) err = pncxrt_memcpy_h2d(dout, hd, (size_t)m * op->ds, s);
+        if (!err) {
+            if (op->kind == PNCXK_SWAP && op->a == 1) {
+                if (dout != din) err = pncxrt_memcpy_d2d(dout, din, (size_t)m, s);
+            } else {
+                err = launch_op(op, din, dout, m, c->dstatus + slot, s);
+            }
+        }
+        if (!err) err = pncxrt_memcpy_d2h(hd, dout, (size_t)m * op->ds, s);
+    }
+    for (i = 0; i < NSLOT; i++) {
+        int e2 = pncxrt_stream_sync(c->stream[i]);
+        if (!err && e2) err = e2;
+    }
+    if (!err) err = pncxrt_memcpy_d2h(&st0, c->dstatus, sizeof(int), c->stream[0]);
+    if (!err) err = pncxrt_memcpy_d2h(&st1, c->dstatus + 1, sizeof(int), c->stream[0]);
+    if (!err) err = pncxrt_stream_sync(c->stream[0]);
+    pthread_mutex_unlock(&c->lock);
+    if (err) return err < 0 ? err : PNCX_EDEVICE;
+    return st0 != 0 ? st0 : st1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* host-buffer entry points                                                  */
+/* ------------------------------------------------------------------------ */
+int pncx_in_swapn(void *buf, pncx_offset nelems, int esize)
+{
+    op_t op;
+    if (esize <= 1 || nelems <= 0) return NC_NOERR;          /* convert_swap.m4:147 */
+    if (!have_device()) return PNCX_EDEVICE;
+    memset(&op, 0, sizeof op);
+    op.kind = PNCXK_SWAP;
+    op.a = esize;
+    op.ss = op.ds = esize;
+    return host_staged(&op, buf, buf, nelems, 0);
+}
+
+int pncx_putn(int cdf_ver, int xtype, void *xbuf, const void *ibuf, pncx_offset nelems,
+              int itype, const void *fillp)
+{
+    op_t op;
+    int err = classify(PNCX_PUT, cdf_ver, xtype, itype, fillp, &op);
+    if (err != NC_NOERR) return err;
+    if (nelems <= 0) return NC_NOERR;
+    if (!have_device()) return PNCX_EDEVICE;
+    return host_staged(&op, ibuf, xbuf, nelems, op.c);
+}
+
+int pncx_getn(int cdf_ver, int xtype, const void *xbuf, void *ibuf, pncx_offset nelems,
+              int itype)
+{
+    op_t op;
+    int err = classify(PNCX_GET, cdf_ver, xtype, itype, NULL, &op);
+    if (err != NC_NOERR) return err;
+    if (nelems <= 0) return NC_NOERR;
+    if (!have_device()) return PNCX_EDEVICE;
+    return host_staged(&op, xbuf, ibuf, nelems, 0);
+}
+
+/* ------------------------------------------------------------------------ */
+/* batched                                                                   */
+/* ------------------------------------------------------------------------ */
+typedef struct bitem_t {
+    op_t        op;
+    int         idx;       /* index into the caller's segs */
+    const void *src;
+    void       *dst;
+    long long   n;
+} bitem_t;
+
+static int cmp_item(const void *pa, const void *pb)
+{
+    const bitem_t *a = (const bitem_t *)pa, *b = (const bitem_t *)pb;
+    if (a->op.kind != b->op.kind) return a->op.kind - b->op.kind;
+    if (a->op.a != b->op.a) return a->op.a - b->op.a;
+    if (a->op.b != b->op.b) return a->op.b - b->op.b;
+    if (a->op.c != b->op.c) return a->op.c - b->op.c;
+    return a->idx - b->idx;
+}
+
+static long long seg_head(const void *src, const void *dst, int ss, int ds, long long n)
+{
+    const uintptr_t s = (uintptr_t)src, d = (uintptr_t)dst;
+    long long h;
+    for (h = 0; h < 16 && h <= n; h++)
+        if (((s + (uintptr_t)h * ss) & 15) == 0 && ((d + (uintptr_t)h * ds) & 15) == 0) return h;
+    return -1;
+}
+
+/* Launch all items (device buffers) grouped by class, statuses into
+ * dstat[idx] (device ints, zeroed by the caller). */
+static int batch_launch(bitem_t *it, int nit, int *dstat, pncxk_seg *dseg, void *stream)
+{
+    int i = 0, err = 0;
+    pncxk_seg *hseg = NULL;
+    qsort(it, (size_t)nit, sizeof *it, cmp_item);
+    hseg = (pncxk_seg *)malloc(sizeof(pncxk_seg) * (size_t)(nit > 0 ? nit : 1));
+    if (hseg == NULL) return NC_ENOMEM;
+    while (!err && i < nit) {
+        int j = i, ns = 0;
+        long long nblocks = 0;
+        pncxk_opinfo oi;
+        const op_t *op = &it[i].op;
+        while (j < nit && it[j].op.kind == op->kind && it[j].op.a == op->a &&
+               it[j].op.b == op->b && it[j].op.c == op->c)
+            j++;
+        if (op->kind == PNCXK_SWAP && op->a == 1) {          /* 1-byte copies */
+            int k;
+            for (k = i; k < j && !err; k++)
+                if (it[k].dst != it[k].src)
+                    err = pncxrt_memcpy_d2d(it[k].dst, it[k].src, (size_t)it[k].n, stream);
+            i = j;
+            continue;
+        }
+        if (op->kind == PNCXK_SWAP && op->a != 2 && op->a != 4 && op->a != 8) {
+            int k;
+            for (k = i; k < j && !err; k++) {
+                pncxk_args a;
+                memset(&a, 0, sizeof a);
+                a.src = it[k].src; a.dst = it[k].dst; a.n = it[k].n; a.stream = stream;
+                err = pncxk_swap_generic(op->a, &a);
+            }
+            i = j;
+            continue;
+        }
+        err = pncxk_opinfo_get(op->kind, op->a, op->b, op->c, &oi);
+        if (err) break;
+        {
+            int k;
+            const long long per_block = (long long)oi.batch_steps * 256;
+            for (k = i; k < j && !err; k++) {
+                const long long h = seg_head(it[k].src, it[k].dst, oi.ss, oi.ds, it[k].n);
+                if (it[k].n <= 0) continue;
+                if (h < 0) {          /* cannot vectorise: own scalar launch */
+                    err = launch_op(&it[k].op, it[k].src, it[k].dst, it[k].n, dstat + it[k].idx, stream);
+                    continue;
+                }
+                hseg[ns].src = it[k].src;
+                hseg[ns].dst = it[k].dst;
+                hseg[ns].n = it[k].n;
+                hseg[ns].head = h;
+                hseg[ns].nvec = (it[k].n - h) / oi.vec;
+                hseg[ns].block0 = nblocks;
+                hseg[ns].fill = it[k].op.fill;
+                hseg[ns].status = dstat + it[k].idx;
+                hseg[ns].pad = 0;
+                nblocks += hseg[ns].nvec > 0 ? (hseg[ns].nvec + per_block - 1) / per_block : 1;
+                ns++;
+            }
+        }
+        if (!err && ns > 0) {
+            pncxk_batch_args ba;
+            /* descriptors of one class live until its kernel ran: keep the
+             * copy and the launch on one stream, and sync before reuse */
+            err = pncxrt_memcpy_h2d(dseg, hseg, sizeof(pncxk_seg) * (size_t)ns, stream);
+            if (!err) {
+                ba.dsegs = dseg;
+                ba.nseg = ns;
+                ba.nblocks = nblocks;
+                ba.stream = stream;
+                err = pncxk_batch(op->kind, op->a, op->b, op->c, &ba);
+            }
+            if (!err) err = pncxrt_stream_sync(stream);
+        }
+        i = j;
+    }
+    free(hseg);
+    return err;
+}
+
+int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_t stream)
+{
+    ctx_t *c;
+    bitem_t *it;
+    int *dstat, *hstat, i, nit = 0, err = 0, first = NC_NOERR;
+    if (nseg <= 0) return NC_NOERR;
+    if (!have_device()) return PNCX_EDEVICE;
+    c = get_ctx();
+    if (c == NULL) return PNCX_EDEVICE;
+    it = (bitem_t *)calloc((size_t)nseg, sizeof *it);
+    hstat = (int *)calloc((size_t)nseg, sizeof(int));
+    if (it == NULL || hstat == NULL) { free(it); free(hstat); return NC_ENOMEM; }
+    for (i = 0; i < nseg; i++) {
+        const pncx_seg *s = &segs[i];
+        int e = classify(s->dir, s->cdf_ver, s->xtype, s->itype, s->fillp, &it[nit].op);
+        if (e != NC_NOERR) { hstat[i] = e; continue; }
+        it[nit].idx = i;
+        it[nit].n = s->nelems;
+        it[nit].src = s->dir == PNCX_PUT ? s->ibuf : s->xbuf;
+        it[nit].dst = s->dir == PNCX_PUT ? s->xbuf : s->ibuf;
+        nit++;
+    }
+    pthread_mutex_lock(&c->lock);
+    err = ensure_scratch(c, ALIGN16(sizeof(int) * (size_t)nseg) + sizeof(pncxk_seg) * (size_t)nseg + 16);
+    dstat = (int *)c->dscratch;
+    if (!err) err = pncxrt_memset(dstat, 0, sizeof(int) * (size_t)nseg, stream);
+    if (!err)
+        err = batch_launch(it, nit, dstat,
+                           (pncxk_seg *)((uint8_t *)c->dscratch + ALIGN16(sizeof(int) * (size_t)nseg)),
+                           stream);
+    if (!err) {
+        int *tmp = (int *)calloc((size_t)nseg, sizeof(int));
+        if (tmp == NULL) err = NC_ENOMEM;
+        if (!err) err = pncxrt_memcpy_d2h(tmp, dstat, sizeof(int) * (size_t)nseg, stream);
+        if (!err) err = pncxrt_stream_sync(stream);
+        if (!err)
+            for (i = 0; i < nseg; i++)
+                if (hstat[i] == NC_NOERR) hstat[i] = tmp[i];
+        free(tmp);
+    }
+    pthread_mutex_unlock(&c->lock);
+    if (!err)
+        for (i = 0; i < nseg; i++) {
+            if (status_out) status_out[i] = hstat[i];
+            if (first == NC_NOERR) first = hstat[i];
+        }
+    free(it);
+    free(hstat);
+    return err ? (err < 0 ? err : PNCX_EDEVICE) : first;
+}
+
+int pncx_batch(const pncx_seg *segs, int nseg, int *status_out)
+{
+    /* Stage every segment into one device arena (16B-aligned slots), run the
+     * device batch, copy the outputs back. */
+    ctx_t *c;
+    pncx_seg *dsegs = NULL;
+    size_t total = 0, off = 0;
+    int i, err = 0, ret;
+    uint8_t *arena = NULL;
+    if (nseg <= 0) return NC_NOERR;
+    if (!have_device()) return PNCX_EDEVICE;
+    c = get_ctx();
+    if (c == NULL) return PNCX_EDEVICE;
+    dsegs = (pncx_seg *)calloc((size_t)nseg, sizeof *dsegs);
+    if (dsegs == NULL) return NC_ENOMEM;
+    for (i = 0; i < nseg; i++) {
+        const int xs = pncx_xlen(segs[i].xtype), is = pncx_ilen(segs[i].itype);
+        if (xs < 0 || is < 0 || segs[i].nelems <= 0) continue;
+        total += ALIGN16((size_t)segs[i].nelems * xs) + ALIGN16((size_t)segs[i].nelems * is);
+    }
+    if (pncxrt_malloc((void **)&arena, total ? total : 16) != 0) { free(dsegs); return PNCX_EDEVICE; }
+    for (i = 0; i < nseg && !err; i++) {
+        const pncx_seg *s = &segs[i];
+        const int xs = pncx_xlen(s->xtype), is = pncx_ilen(s->itype);
+        dsegs[i] = *s;
+        if (xs < 0 || is < 0 || s->nelems <= 0) continue;
+        dsegs[i].xbuf = arena + off;
+        off += ALIGN16((size_t)s->nelems * xs);
+        dsegs[i].ibuf = arena + off;
+        off += ALIGN16((size_t)s->nelems * is);
+        if (s->dir == PNCX_PUT) {
+            err = pncxrt_memcpy_h2d(dsegs[i].ibuf, s->ibuf, (size_t)s->nelems * is, c->stream[0]);
+            if (!err && s->fillp == NULL)   /* NULL-fill codecs read xbuf */
+                err = pncxrt_memcpy_h2d(dsegs[i].xbuf, s->xbuf, (size_t)s->nelems * xs, c->stream[0]);
+        } else {
+            err = pncxrt_memcpy_h2d(dsegs[i].xbuf, s->xbuf, (size_t)s->nelems * xs, c->stream[0]);
+        }
+    }
+    ret = err ? PNCX_EDEVICE : pncx_dev_batch(dsegs, nseg, status_out, c->stream[0]);
+    for (i = 0; i < nseg && !err; i++) {
+        const pncx_seg *s = &segs[i];
+        const int xs = pncx_xlen(s->xtype), is = pncx_ilen(s->itype);
+        if (xs < 0 || is < 0 || s->nelems <= 0) continue;
+        if (s->dir == PNCX_PUT)
+            err = pncxrt_memcpy_d2h(s->xbuf, dsegs[i].xbuf, (size_t)s->nelems * xs, c->stream[0]);
+        else
+            err = pncxrt_memcpy_d2h(s->ibuf, dsegs[i].ibuf, (size_t)s->nelems * is, c->stream[0]);
+    }
+    if (!err) err = pncxrt_stream_sync(c->stream[0]);
+    pncxrt_free(arena);
+    free(dsegs);
+    if (err) return PNCX_EDEVICE;
+    return ret;
+}

@@ -1,0 +1,322 @@
+// pncx_kern.hpp -- streaming kernels of the swap / type-convert path (gfx950).
+//
+// One kernel template serves every conversion class.  An "Op" says how one
+// source element (raw bits as loaded) becomes one destination element (raw
+// bits as stored) and how many elements a lane handles per step (VEC, chosen
+// so the narrower side moves exactly 16 bytes).  Per step a lane issues
+// global_load_dwordx4 / global_store_dwordx4 on its own 16-byte-aligned
+// slice, so a wave moves 1 KiB per instruction, fully coalesced; UNROLL steps
+// are loaded before any is stored to keep several KiB in flight per wave.
+// The kernel is HBM-bound (no contraction: no MFMA, no LDS).
+//
+// Status: a lane accumulates "some element was out of range"; at the end the
+// wave ballots it and one lane stores NC_ERANGE into *status.  This is the
+// reference's "return the first error" (ncx.m4:2487-2488) since NC_ERANGE is
+// the only error a conversion loop can produce.
+#pragma once
+
+#include "pncx_device.hpp"
+#include "pncx_shim.h"
+
+namespace pncx {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const uint8_t *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    else return *reinterpret_cast<const u32x4 *>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st16(uint8_t *p, u32x4 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+    else *reinterpret_cast<u32x4 *>(p) = v;
+}
+
+template <typename T>
+__device__ __forceinline__ T ld_unaligned(const uint8_t *p) {
+    T t;
+    __builtin_memcpy(&t, p, sizeof t);
+    return t;
+}
+template <typename T>
+__device__ __forceinline__ void st_unaligned(uint8_t *p, T t) {
+    __builtin_memcpy(p, &t, sizeof t);
+}
+
+template <int A, int B> struct cmin { static constexpr int value = A < B ? A : B; };
+
+// ---------------------------------------------------------------------------
+// Ops
+// ---------------------------------------------------------------------------
+// byte reversal of ES-byte elements (ncmpii_in_swapn / swapn?b)
+template <int ES>
+struct SwapOp {
+    using SU = typename std::conditional<ES == 1, uint8_t,
+               typename std::conditional<ES == 2, uint16_t,
+               typename std::conditional<ES == 4, uint32_t, uint64_t>::type>::type>::type;
+    using DU = SU;
+    using fill_t = uint64_t;
+    static constexpr int SS = ES, DS = ES, VEC = 16 / ES;
+    static constexpr bool PRESERVE = false;
+    __device__ static __forceinline__ DU one(SU s, DU, fill_t, bool &) { return bswap(s); }
+};
+
+// GET: external (big-endian raw) -> internal (native raw)
+template <int XT, int IT>
+struct GetOp {
+    using XI = X<XT>;
+    using II = I<IT>;
+    using SU = typename XI::U;
+    using DU = typename II::U;
+    using fill_t = uint64_t;
+    static constexpr int SS = XI::size, DS = II::size;
+    static constexpr int VEC = 16 / cmin<SS, DS>::value;
+    static constexpr bool PRESERVE = false;
+    __device__ static __forceinline__ DU one(SU s, DU, fill_t, bool &bad) {
+        const typename XI::T xx = bits_to<typename XI::T>(bswap(s));
+        const typename II::T v = get1<XT, IT>(xx, bad);
+        return bits_to<DU>(v);
+    }
+};
+
+// PUT: internal (native raw) -> external (big-endian raw)
+template <int XT, int IT, bool PRES>
+struct PutOp {
+    using XI = X<XT>;
+    using II = I<IT>;
+    using SU = typename II::U;
+    using DU = typename XI::U;
+    using fill_t = uint64_t;   // native bits of the xtype fill value
+    static constexpr int SS = II::size, DS = XI::size;
+    static constexpr int VEC = 16 / cmin<SS, DS>::value;
+    static constexpr bool PRESERVE = PRES;
+    __device__ static __forceinline__ DU one(SU s, DU old, fill_t fill, bool &bad) {
+        const typename II::T v = bits_to<typename II::T>(s);
+        bool b = false;
+        const typename XI::T xx = put1<XT, IT>(v, bits_to<typename XI::T>((DU)fill), b);
+        bad |= b;
+        if constexpr (PRES) {
+            // fillp == NULL: keep (1-byte) or swap (ushort/uint <- schar) the
+            // bytes already in xbuf
+            if (b) return bswap(old);
+        }
+        return bswap(bits_to<DU>(xx));
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Kernel: vector body over 16B-aligned [head, head + nvec*VEC) plus scalar
+// head [0, head) and tail [head + nvec*VEC, n).
+// ---------------------------------------------------------------------------
+template <class Op>
+__device__ __forceinline__ void scalar_elem(const uint8_t *src, uint8_t *dst, int64_t e,
+                                            typename Op::fill_t fill, bool &bad) {
+    using SU = typename Op::SU;
+    using DU = typename Op::DU;
+    const SU s = ld_unaligned<SU>(src + e * Op::SS);
+    DU old = 0;
+    if constexpr (Op::PRESERVE) old = ld_unaligned<DU>(dst + e * Op::DS);
+    st_unaligned<DU>(dst + e * Op::DS, Op::one(s, old, fill, bad));
+}
+
+template <class Op, bool NT>
+__device__ __forceinline__ void vec_step(const uint8_t *src, uint8_t *dst,
+                                         typename Op::fill_t fill, bool &bad) {
+    constexpr int SB = Op::VEC * Op::SS, DB = Op::VEC * Op::DS;
+    constexpr int NS = SB / 16, ND = DB / 16;
+    using SU = typename Op::SU;
+    using DU = typename Op::DU;
+    u32x4 sv[NS];
+#pragma unroll
+    for (int k = 0; k < NS; k++) sv[k] = ld16<NT>(src + 16 * k);
+    u32x4 ov[ND];
+    if constexpr (Op::PRESERVE) {
+#pragma unroll
+        for (int k = 0; k < ND; k++) ov[k] = ld16<false>(dst + 16 * k);
+    }
+    SU s[Op::VEC];
+    DU d[Op::VEC];
+    __builtin_memcpy(s, sv, SB);
+    if constexpr (Op::PRESERVE) __builtin_memcpy(d, ov, DB);
+#pragma unroll
+    for (int e = 0; e < Op::VEC; e++) d[e] = Op::one(s[e], d[e], fill, bad);
+    __builtin_memcpy(ov, d, DB);
+#pragma unroll
+    for (int k = 0; k < ND; k++) st16<NT>(dst + 16 * k, ov[k]);
+}
+
+__device__ __forceinline__ void publish_status(int *status, bool bad) {
+    const unsigned long long m = __ballot(bad);
+    if (m != 0 && status != nullptr && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)m) - 1))
+        __hip_atomic_store(status, NC_ERANGE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <class Op, int UNROLL, bool NT>
+__global__ __launch_bounds__(256) void k_stream(const uint8_t *src, uint8_t *dst, int64_t head,
+                                                int64_t nvec, int64_t n,
+                                                typename Op::fill_t fill, int *status) {
+    constexpr int SB = Op::VEC * Op::SS, DB = Op::VEC * Op::DS;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    bool bad = false;
+
+    // scalar head / tail (a few elements)
+    const int64_t tail0 = head + nvec * Op::VEC;
+    if (tid < head) scalar_elem<Op>(src, dst, tid, fill, bad);
+    if (tail0 + tid < n) scalar_elem<Op>(src, dst, tail0 + tid, fill, bad);
+
+    const uint8_t *vs = src + head * Op::SS;
+    uint8_t *vd = dst + head * Op::DS;
+    int64_t v = tid;
+    for (; v + (UNROLL - 1) * stride < nvec; v += UNROLL * stride) {
+        if constexpr (UNROLL == 1) {
+            vec_step<Op, NT>(vs + v * SB, vd + v * DB, fill, bad);
+        } else {
+            // all loads of the UNROLL steps first, then convert + store
+            constexpr int NS = SB / 16, ND = DB / 16;
+            using SU = typename Op::SU;
+            using DU = typename Op::DU;
+            u32x4 sv[UNROLL][NS];
+#pragma unroll
+            for (int u = 0; u < UNROLL; u++)
+#pragma unroll
+                for (int k = 0; k < NS; k++) sv[u][k] = ld16<NT>(vs + (v + u * stride) * SB + 16 * k);
+            u32x4 ov[UNROLL][ND];
+            if constexpr (Op::PRESERVE) {
+#pragma unroll
+                for (int u = 0; u < UNROLL; u++)
+#pragma unroll
+                    for (int k = 0; k < ND; k++) ov[u][k] = ld16<false>(vd + (v + u * stride) * DB + 16 * k);
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL; u++) {
+                SU s[Op::VEC];
+                DU d[Op::VEC];
+                __builtin_memcpy(s, sv[u], SB);
+                if constexpr (Op::PRESERVE) __builtin_memcpy(d, ov[u], DB);
+#pragma unroll
+                for (int e = 0; e < Op::VEC; e++) d[e] = Op::one(s[e], d[e], fill, bad);
+                __builtin_memcpy(ov[u], d, DB);
+#pragma unroll
+                for (int k = 0; k < ND; k++) st16<NT>(vd + (v + u * stride) * DB + 16 * k, ov[u][k]);
+            }
+        }
+    }
+    for (; v < nvec; v += stride) vec_step<Op, NT>(vs + v * SB, vd + v * DB, fill, bad);
+
+    publish_status(status, bad);
+}
+
+// fully scalar (misaligned buffers): one element per lane, byte-wise access
+template <class Op>
+__global__ __launch_bounds__(256) void k_scalar(const uint8_t *src, uint8_t *dst, int64_t n,
+                                                typename Op::fill_t fill, int *status) {
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    bool bad = false;
+    for (int64_t e = tid; e < n; e += stride) scalar_elem<Op>(src, dst, e, fill, bad);
+    publish_status(status, bad);
+}
+
+// ---------------------------------------------------------------------------
+// Batched: many segments of one class in one launch.  Block b serves segment
+// s with seg[s].block0 <= b < seg[s+1].block0 and handles a contiguous run of
+// BATCH_STEPS vector steps of it (thread-strided inside the block, so each
+// wave-instruction still moves 1 KiB contiguously).
+// ---------------------------------------------------------------------------
+constexpr int BATCH_STEPS = 8;  // vector steps per lane per block
+
+template <class Op, bool NT>
+__global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg) {
+    constexpr int SB = Op::VEC * Op::SS, DB = Op::VEC * Op::DS;
+    // binary search for the segment of this block (segs sorted by block0)
+    const long long b = blockIdx.x;
+    int lo = 0, hi = nseg - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (segs[mid].block0 <= b) lo = mid; else hi = mid - 1;
+    }
+    const pncxk_seg sg = segs[lo];
+    const uint8_t *src = (const uint8_t *)sg.src;
+    uint8_t *dst = (uint8_t *)sg.dst;
+    const typename Op::fill_t fill = sg.fill;
+    const int64_t nvec = sg.nvec;
+    bool bad = false;
+
+    const int64_t rel = b - sg.block0;
+    if (rel == 0) {  // first block of the segment: scalar head and tail
+        const int64_t tail0 = sg.head + nvec * Op::VEC;
+        if (threadIdx.x < sg.head) scalar_elem<Op>(src, dst, threadIdx.x, fill, bad);
+        if (tail0 + threadIdx.x < sg.n) scalar_elem<Op>(src, dst, tail0 + threadIdx.x, fill, bad);
+    }
+    const uint8_t *vs = src + sg.head * Op::SS;
+    uint8_t *vd = dst + sg.head * Op::DS;
+    const int64_t v0 = rel * (int64_t)(BATCH_STEPS * 256);
+#pragma unroll
+    for (int u = 0; u < BATCH_STEPS; u++) {
+        const int64_t v = v0 + u * 256 + threadIdx.x;
+        if (v < nvec) vec_step<Op, NT>(vs + v * SB, vd + v * DB, fill, bad);
+    }
+    publish_status(sg.status, bad);
+}
+
+// ---------------------------------------------------------------------------
+// host-side helpers
+// ---------------------------------------------------------------------------
+// Elements before both pointers are 16B-aligned; -1 if no such split exists.
+template <class Op>
+inline int64_t vec_head(const void *src, const void *dst, int64_t n) {
+    const uintptr_t s = (uintptr_t)src, d = (uintptr_t)dst;
+    for (int64_t h = 0; h < 16 && h <= n; h++)
+        if (((s + h * Op::SS) & 15) == 0 && ((d + h * Op::DS) & 15) == 0) return h;
+    return -1;
+}
+
+int launch_grid(int64_t work_items, int per_thread);  // defined in pncx_kern_swap.hip
+
+template <class Op>
+int launch_stream(const pncxk_args *a) {
+    hipStream_t st = (hipStream_t)a->stream;
+    const int64_t n = a->n;
+    if (n <= 0) return 0;
+    const int64_t h = vec_head<Op>(a->src, a->dst, n);
+    const uint8_t *src = (const uint8_t *)a->src;
+    uint8_t *dst = (uint8_t *)a->dst;
+    if (h < 0) {
+        const int grid = launch_grid(n, 1);
+        hipLaunchKernelGGL((k_scalar<Op>), dim3(grid), dim3(256), 0, st, src, dst, n,
+                           (typename Op::fill_t)a->fill, a->status);
+    } else {
+        const int64_t nvec = (n - h) / Op::VEC;
+        constexpr int U = (Op::VEC * Op::SS + Op::VEC * Op::DS) <= 48 ? 4 : 2;
+        const int grid = launch_grid(nvec > 0 ? nvec : 1, U);
+        if (a->nontemporal)
+            hipLaunchKernelGGL((k_stream<Op, U, true>), dim3(grid), dim3(256), 0, st, src, dst, h,
+                               nvec, n, (typename Op::fill_t)a->fill, a->status);
+        else
+            hipLaunchKernelGGL((k_stream<Op, U, false>), dim3(grid), dim3(256), 0, st, src, dst,
+                               h, nvec, n, (typename Op::fill_t)a->fill, a->status);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
+}
+
+template <class Op>
+int launch_batch(const pncxk_batch_args *a) {
+    if (a->nblocks <= 0) return 0;
+    hipLaunchKernelGGL((k_batch<Op, false>), dim3((unsigned)a->nblocks), dim3(256), 0,
+                       (hipStream_t)a->stream, a->dsegs, a->nseg);
+    return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
+}
+
+template <class Op>
+struct OpInfo {
+    static void fill(pncxk_opinfo *o) {
+        o->ss = Op::SS;
+        o->ds = Op::DS;
+        o->vec = Op::VEC;
+        o->batch_steps = BATCH_STEPS;
+    }
+};
+
+}  // namespace pncx

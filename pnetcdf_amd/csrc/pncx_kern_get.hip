@@ -1,0 +1,53 @@
+// pncx_kern_get.hip -- GET kernels: external (XDR big-endian) -> internal,
+// one instance per (xtype, itype) of ncmpix_getn_NC_<X>_<itype>
+// (ncx.m4 NCX_GETN :2429-2495 / NCX_GETN_BYTE :2369-2392).
+#include "pncx_pairs.hpp"
+
+using namespace pncx;
+
+namespace {
+template <int XT, int IT>
+int get_one(const pncxk_args *a) {
+    if constexpr (same_rep<XT, IT>::value) return NC_EINVAL;
+    else return launch_stream<GetOp<XT, IT>>(a);
+}
+template <int XT, int IT>
+int get_batch(const pncxk_batch_args *a) {
+    if constexpr (same_rep<XT, IT>::value) return NC_EINVAL;
+    else return launch_batch<GetOp<XT, IT>>(a);
+}
+template <int XT, int IT>
+int get_info(pncxk_opinfo *o) {
+    OpInfo<GetOp<XT, IT>>::fill(o);
+    return 0;
+}
+}  // namespace
+
+#define PNCX_KEY(XT, IT) ((XT) * 16 + (IT))
+
+extern "C" int pncxk_get(int xtype, int itype, const pncxk_args *a) {
+    switch (PNCX_KEY(xtype, itype)) {
+#define CASE(XT, IT) case PNCX_KEY(XT, IT): return get_one<XT, IT>(a);
+        PNCX_ALL_PAIRS(CASE)
+#undef CASE
+        default: return NC_EBADTYPE;
+    }
+}
+
+extern "C" int pncxk_batch_get(int xtype, int itype, const pncxk_batch_args *a) {
+    switch (PNCX_KEY(xtype, itype)) {
+#define CASE(XT, IT) case PNCX_KEY(XT, IT): return get_batch<XT, IT>(a);
+        PNCX_ALL_PAIRS(CASE)
+#undef CASE
+        default: return NC_EBADTYPE;
+    }
+}
+
+extern "C" int pncxk_opinfo_get_get(int xtype, int itype, pncxk_opinfo *o) {
+    switch (PNCX_KEY(xtype, itype)) {
+#define CASE(XT, IT) case PNCX_KEY(XT, IT): return get_info<XT, IT>(o);
+        PNCX_ALL_PAIRS(CASE)
+#undef CASE
+        default: return NC_EBADTYPE;
+    }
+}

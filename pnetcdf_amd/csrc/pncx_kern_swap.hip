@@ -1,0 +1,187 @@
+// pncx_kern_swap.hip -- byte-swap / copy launchers, the generic n-byte swap
+// kernel, grid sizing, batch dispatch, and the thin HIP-runtime wrappers that
+// the C host code (pncx_host.c) calls.
+#include <stdlib.h>
+#include <string.h>
+
+#include "pncx_kern.hpp"
+
+using namespace pncx;
+
+// ---------------------------------------------------------------------------
+// grid sizing: memory-bound streaming -> enough blocks to fill 256 CUs
+// (8 XCDs x 32 CUs) several times, grid-stride the rest.
+// ---------------------------------------------------------------------------
+static int g_cu_count[64];
+
+static int cu_count() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (g_cu_count[dev] == 0) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+        g_cu_count[dev] = cus;
+    }
+    return g_cu_count[dev];
+}
+
+static int blocks_per_cu() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("PNCX_BLOCKS_PER_CU");
+        v = (e && atoi(e) > 0) ? atoi(e) : 8;
+    }
+    return v;
+}
+
+namespace pncx {
+int launch_grid(int64_t work_items, int per_thread) {
+    const int64_t want = (work_items + 256LL * per_thread - 1) / (256LL * per_thread);
+    const int64_t cap = (int64_t)cu_count() * blocks_per_cu();
+    int64_t g = want < cap ? want : cap;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+}  // namespace pncx
+
+// ---------------------------------------------------------------------------
+// generic esize (not 1/2/4/8): one element per lane, byte reversal
+// (ncmpii_in_swapn generic branch, convert_swap.m4:184-195)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_swap_generic(const uint8_t *src, uint8_t *dst, int64_t n,
+                                                      int esize) {
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = tid; e < n; e += stride) {
+        const uint8_t *s = src + e * esize;
+        uint8_t *d = dst + e * esize;
+        for (int i = 0; i < esize / 2; i++) {
+            const uint8_t a = s[i], b = s[esize - 1 - i];
+            d[i] = b;
+            d[esize - 1 - i] = a;
+        }
+        if (esize & 1) d[esize / 2] = s[esize / 2];
+    }
+}
+
+extern "C" int pncxk_swap(int esize, const pncxk_args *a) {
+    switch (esize) {
+        case 1: return launch_stream<SwapOp<1>>(a);
+        case 2: return launch_stream<SwapOp<2>>(a);
+        case 4: return launch_stream<SwapOp<4>>(a);
+        case 8: return launch_stream<SwapOp<8>>(a);
+        default: return pncxk_swap_generic(esize, a);
+    }
+}
+
+extern "C" int pncxk_swap_generic(int esize, const pncxk_args *a) {
+    if (a->n <= 0 || esize <= 0) return 0;
+    const int grid = launch_grid(a->n, 1);
+    hipLaunchKernelGGL(k_swap_generic, dim3(grid), dim3(256), 0, (hipStream_t)a->stream,
+                       (const uint8_t *)a->src, (uint8_t *)a->dst, (int64_t)a->n, esize);
+    return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
+}
+
+// batch / opinfo dispatch: get and put live in their own TUs
+extern "C" int pncxk_batch_get(int xtype, int itype, const pncxk_batch_args *a);
+extern "C" int pncxk_batch_put(int xtype, int itype, int preserve, const pncxk_batch_args *a);
+extern "C" int pncxk_opinfo_getput(int kind, int xtype, int itype, int preserve, pncxk_opinfo *o);
+
+extern "C" int pncxk_batch(int kind, int a, int b, int c, const pncxk_batch_args *args) {
+    if (kind == PNCXK_SWAP) {
+        switch (a) {
+            case 1: return launch_batch<SwapOp<1>>(args);
+            case 2: return launch_batch<SwapOp<2>>(args);
+            case 4: return launch_batch<SwapOp<4>>(args);
+            case 8: return launch_batch<SwapOp<8>>(args);
+            default: return NC_EINVAL;
+        }
+    }
+    if (kind == PNCXK_GET) return pncxk_batch_get(a, b, args);
+    if (kind == PNCXK_PUT) return pncxk_batch_put(a, b, c, args);
+    return NC_EINVAL;
+}
+
+extern "C" int pncxk_opinfo_get(int kind, int a, int b, int c, pncxk_opinfo *o) {
+    if (kind == PNCXK_SWAP) {
+        switch (a) {
+            case 1: OpInfo<SwapOp<1>>::fill(o); return 0;
+            case 2: OpInfo<SwapOp<2>>::fill(o); return 0;
+            case 4: OpInfo<SwapOp<4>>::fill(o); return 0;
+            case 8: OpInfo<SwapOp<8>>::fill(o); return 0;
+            default: return NC_EINVAL;
+        }
+    }
+    return pncxk_opinfo_getput(kind, a, b, c, o);
+}
+
+// ---------------------------------------------------------------------------
+// HIP runtime wrappers
+// ---------------------------------------------------------------------------
+static thread_local char g_last_err[256];
+
+static int rt(hipError_t e, const char *what) {
+    if (e == hipSuccess) return 0;
+    snprintf(g_last_err, sizeof g_last_err, "%s: %s", what, hipGetErrorString(e));
+    return PNCX_EDEVICE;
+}
+
+extern "C" {
+const char *pncxrt_last_error(void) { return g_last_err; }
+int pncxrt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+int pncxrt_set_device(int dev) { return rt(hipSetDevice(dev), "hipSetDevice"); }
+int pncxrt_get_device(void) {
+    int d = -1;
+    if (hipGetDevice(&d) != hipSuccess) return -1;
+    return d;
+}
+int pncxrt_malloc(void **p, size_t n) { return rt(hipMalloc(p, n ? n : 1), "hipMalloc"); }
+int pncxrt_free(void *p) { return p ? rt(hipFree(p), "hipFree") : 0; }
+int pncxrt_host_alloc(void **p, size_t n) {
+    return rt(hipHostMalloc(p, n ? n : 1, hipHostMallocDefault), "hipHostMalloc");
+}
+int pncxrt_host_free(void *p) { return p ? rt(hipHostFree(p), "hipHostFree") : 0; }
+int pncxrt_memcpy_h2d(void *d, const void *h, size_t n, void *s) {
+    return rt(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, (hipStream_t)s), "hipMemcpyAsync H2D");
+}
+int pncxrt_memcpy_d2h(void *h, const void *d, size_t n, void *s) {
+    return rt(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, (hipStream_t)s), "hipMemcpyAsync D2H");
+}
+int pncxrt_memcpy_d2d(void *d, const void *src, size_t n, void *s) {
+    return rt(hipMemcpyAsync(d, src, n, hipMemcpyDeviceToDevice, (hipStream_t)s), "hipMemcpyAsync D2D");
+}
+int pncxrt_memset(void *d, int v, size_t n, void *s) {
+    return rt(hipMemsetAsync(d, v, n, (hipStream_t)s), "hipMemsetAsync");
+}
+int pncxrt_stream_create(void **s) {
+    return rt(hipStreamCreateWithFlags((hipStream_t *)s, hipStreamNonBlocking), "hipStreamCreate");
+}
+int pncxrt_stream_destroy(void *s) { return s ? rt(hipStreamDestroy((hipStream_t)s), "hipStreamDestroy") : 0; }
+int pncxrt_stream_sync(void *s) { return rt(hipStreamSynchronize((hipStream_t)s), "hipStreamSynchronize"); }
+int pncxrt_event_create(void **e) { return rt(hipEventCreate((hipEvent_t *)e), "hipEventCreate"); }
+int pncxrt_event_destroy(void *e) { return e ? rt(hipEventDestroy((hipEvent_t)e), "hipEventDestroy") : 0; }
+int pncxrt_event_record(void *e, void *s) {
+    return rt(hipEventRecord((hipEvent_t)e, (hipStream_t)s), "hipEventRecord");
+}
+int pncxrt_stream_wait_event(void *s, void *e) {
+    return rt(hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)e, 0), "hipStreamWaitEvent");
+}
+int pncxrt_event_sync(void *e) { return rt(hipEventSynchronize((hipEvent_t)e), "hipEventSynchronize"); }
+int pncxrt_event_elapsed_ms(float *ms, void *a, void *b) {
+    return rt(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b), "hipEventElapsedTime");
+}
+int pncxrt_is_device_ptr(const void *p) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return at.type == hipMemoryTypeDevice;
+}
+}  // extern "C"

@@ -1,0 +1,93 @@
+/*
+ * pncx_shim.h -- the thin C-ABI between the C host code (pncx_host.c) and
+ * the HIP translation units (kernel launchers + HIP runtime wrappers).
+ * Internal to libpncx.so; the public boundary is include/pncx.h.
+ */
+#ifndef PNCX_SHIM_H
+#define PNCX_SHIM_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* one streaming launch: n elements from src to dst (may be equal) */
+typedef struct pncxk_args {
+    const void        *src;
+    void              *dst;
+    long long          n;
+    unsigned long long fill;        /* PUT: native bits of the xtype fill */
+    int               *status;      /* device int or NULL                 */
+    void              *stream;      /* hipStream_t                        */
+    int                nontemporal; /* 1: nt loads/stores                 */
+} pncxk_args;
+
+/* one segment of a batched launch (device-resident copy of this array) */
+typedef struct pncxk_seg {
+    const void        *src;
+    void              *dst;
+    long long          n;
+    long long          head;   /* scalar elements before the 16B-aligned body */
+    long long          nvec;   /* vector steps in the body                    */
+    long long          block0; /* first block of this segment                 */
+    unsigned long long fill;
+    int               *status; /* device int of this segment, or NULL         */
+    int                pad;
+} pncxk_seg;
+
+typedef struct pncxk_batch_args {
+    const pncxk_seg *dsegs;    /* device array, sorted by block0 */
+    int              nseg;
+    long long        nblocks;
+    void            *stream;
+} pncxk_batch_args;
+
+typedef struct pncxk_opinfo {
+    int ss;           /* source element bytes       */
+    int ds;           /* destination element bytes  */
+    int vec;          /* elements per lane per step */
+    int batch_steps;  /* steps per lane per block   */
+} pncxk_opinfo;
+
+/* operation kinds for batch / opinfo */
+#define PNCXK_SWAP 0  /* a = esize (1 = copy)  */
+#define PNCXK_GET  1  /* a = xtype, b = itype  */
+#define PNCXK_PUT  2  /* a = xtype, b = itype, c = preserve */
+
+/* ---- kernel launchers (HIP TUs) ---- */
+int pncxk_swap(int esize, const pncxk_args *a);          /* esize 1,2,4,8 */
+int pncxk_swap_generic(int esize, const pncxk_args *a);  /* any esize >= 1 */
+int pncxk_get(int xtype, int itype, const pncxk_args *a);
+int pncxk_put(int xtype, int itype, int preserve, const pncxk_args *a);
+int pncxk_batch(int kind, int a, int b, int c, const pncxk_batch_args *args);
+int pncxk_opinfo_get(int kind, int a, int b, int c, pncxk_opinfo *o);
+
+/* ---- HIP runtime wrappers (return 0 on success, PNCX_EDEVICE on error) ---- */
+int  pncxrt_device_count(void);
+int  pncxrt_set_device(int dev);
+int  pncxrt_get_device(void);
+int  pncxrt_malloc(void **p, size_t n);
+int  pncxrt_free(void *p);
+int  pncxrt_host_alloc(void **p, size_t n);
+int  pncxrt_host_free(void *p);
+int  pncxrt_memcpy_h2d(void *d, const void *h, size_t n, void *stream);
+int  pncxrt_memcpy_d2h(void *h, const void *d, size_t n, void *stream);
+int  pncxrt_memcpy_d2d(void *d, const void *s, size_t n, void *stream);
+int  pncxrt_memset(void *d, int v, size_t n, void *stream);
+int  pncxrt_stream_create(void **s);
+int  pncxrt_stream_destroy(void *s);
+int  pncxrt_stream_sync(void *s);
+int  pncxrt_event_create(void **e);
+int  pncxrt_event_destroy(void *e);
+int  pncxrt_event_record(void *e, void *stream);
+int  pncxrt_stream_wait_event(void *stream, void *e);
+int  pncxrt_event_sync(void *e);
+int  pncxrt_event_elapsed_ms(float *ms, void *start, void *stop);
+int  pncxrt_is_device_ptr(const void *p);
+const char *pncxrt_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

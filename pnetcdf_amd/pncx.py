@@ -1,0 +1,209 @@
+"""Python mirror of PnetCDF's conversion interface over the HIP C-ABI.
+
+Names follow the reference (src/drivers/include/common.h:147-221):
+``need_convert``, ``in_swapn``, ``putn``, ``getn`` operate on host (numpy)
+buffers exactly like ncmpii_need_convert / ncmpii_in_swapn /
+ncmpii_putn_NC_<X> / ncmpii_getn_NC_<X>; the ``dev_*`` variants operate on
+HBM-resident torch tensors.  Every call goes to ``pnetcdf_amd/lib/libpncx.so``
+(the HIP kernels).  There is no CPU fallback: if the library or a GPU is
+missing, calls raise.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import nctypes as T
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(_HERE, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libpncx.so")
+_lib = None
+
+
+class PncxError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        super().__init__(f"{what}: {strerror(code)} ({code})" if what else f"{strerror(code)} ({code})")
+
+
+def lib():
+    """Load the in-tree libpncx.so.  torch is imported first (when present)
+    so that the library binds to the same HIP runtime instance as torch."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:
+        import torch  # noqa: F401  (share one HIP runtime with torch)
+    except ImportError:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise PncxError(T.PNCX_EDEVICE, f"{LIB_PATH} not built (run __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    vp, ll, i = ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int
+    sig = {
+        "pncx_xlen": (i, [i]), "pncx_ilen": (i, [i]),
+        "pncx_need_convert": (i, [i, i, i]), "pncx_need_swap": (i, [i, i]),
+        "pncx_in_swapn": (i, [vp, ll, i]),
+        "pncx_putn": (i, [i, i, vp, vp, ll, i, vp]),
+        "pncx_getn": (i, [i, i, vp, vp, ll, i]),
+        "pncx_dev_in_swapn": (i, [vp, ll, i, vp]),
+        "pncx_dev_swapn": (i, [vp, vp, ll, i, vp]),
+        "pncx_dev_putn": (i, [i, i, vp, vp, ll, i, vp, vp, vp]),
+        "pncx_dev_getn": (i, [i, i, vp, vp, ll, i, vp, vp]),
+        "pncx_dev_batch": (i, [vp, i, vp, vp]),
+        "pncx_batch": (i, [vp, i, vp]),
+        "pncx_device_count": (i, []), "pncx_set_device": (i, [i]),
+        "pncx_get_device": (i, []),
+        "pncx_dev_status_read": (i, [vp, vp]),
+        "pncx_strerror": (ctypes.c_char_p, [i]),
+        "pncx_version": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def strerror(code):
+    try:
+        return lib().pncx_strerror(code).decode()
+    except Exception:  # library not loadable
+        return f"error {code}"
+
+
+def version():
+    return lib().pncx_version().decode()
+
+
+def device_count():
+    return lib().pncx_device_count()
+
+
+class Seg(ctypes.Structure):
+    """struct pncx_seg (include/pncx.h)"""
+    _fields_ = [("dir", ctypes.c_int), ("cdf_ver", ctypes.c_int), ("xtype", ctypes.c_int),
+                ("itype", ctypes.c_int), ("nelems", ctypes.c_longlong),
+                ("xbuf", ctypes.c_void_p), ("ibuf", ctypes.c_void_p), ("fillp", ctypes.c_void_p)]
+
+
+def _np_ptr(a):
+    assert isinstance(a, np.ndarray) and a.flags["C_CONTIGUOUS"]
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _check(code, what, allow=(T.NC_NOERR, T.NC_ERANGE)):
+    if code not in allow:
+        raise PncxError(code, what)
+    return code
+
+
+# ---------------------------------------------------------------- host side
+def need_convert(fmt, xtype, itype):
+    """ncmpii_need_convert (convert_swap.m4:85-116)"""
+    return lib().pncx_need_convert(fmt, xtype, itype)
+
+
+def need_swap(xtype, itype):
+    """NEED_BYTE_SWAP (common.h:47-54)"""
+    return lib().pncx_need_swap(xtype, itype)
+
+
+def in_swapn(buf, nelems, esize):
+    """ncmpii_in_swapn (convert_swap.m4:137-197) on a host numpy buffer."""
+    _check(lib().pncx_in_swapn(_np_ptr(buf), nelems, esize), "in_swapn", (T.NC_NOERR,))
+
+
+def putn(cdf_ver, xtype, xbuf, ibuf, nelems, itype, fillp=None):
+    """ncmpii_putn_NC_<X>: ibuf (itype) -> xbuf (big-endian xtype).
+    fillp: bytes of the xtype fill value in native order, or None (NULL).
+    Returns NC_NOERR or NC_ERANGE; raises on any other status."""
+    fb = None if fillp is None else np.frombuffer(bytes(fillp) + b"\0" * 8, np.uint8).copy()
+    return _check(lib().pncx_putn(cdf_ver, xtype, _np_ptr(xbuf), _np_ptr(ibuf), nelems, itype,
+                                  None if fb is None else _np_ptr(fb)), "putn")
+
+
+def getn(cdf_ver, xtype, xbuf, ibuf, nelems, itype):
+    """ncmpii_getn_NC_<X>: xbuf (big-endian xtype) -> ibuf (itype)."""
+    return _check(lib().pncx_getn(cdf_ver, xtype, _np_ptr(xbuf), _np_ptr(ibuf), nelems, itype),
+                  "getn")
+
+
+def batch(segs):
+    """Host-buffer batch: segs = list of dicts with dir, cdf_ver, xtype,
+    itype, nelems, xbuf, ibuf (numpy), fill (bytes or None).  Returns the
+    per-segment status list."""
+    arr = (Seg * len(segs))()
+    keep = []
+    for k, s in enumerate(segs):
+        fb = None
+        if s.get("fill") is not None:
+            fb = np.frombuffer(bytes(s["fill"]) + b"\0" * 8, np.uint8).copy()
+            keep.append(fb)
+        arr[k] = Seg(s["dir"], s.get("cdf_ver", 5), s["xtype"], s["itype"], s["nelems"],
+                     s["xbuf"].ctypes.data, s["ibuf"].ctypes.data,
+                     None if fb is None else fb.ctypes.data)
+    st = (ctypes.c_int * len(segs))()
+    rc = lib().pncx_batch(arr, len(segs), st)
+    if rc not in (T.NC_NOERR, T.NC_ERANGE, T.NC_EBADTYPE, T.NC_ECHAR):
+        raise PncxError(rc, "batch")
+    return list(st)
+
+
+# -------------------------------------------------------------- device side
+def _stream_ptr(stream):
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def _dptr(t):
+    assert t.is_cuda and t.is_contiguous()
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def dev_in_swapn(t, nelems, esize, stream=None):
+    """In-place swap of an HBM tensor (the config-2/5 hot kernel)."""
+    _check(lib().pncx_dev_in_swapn(_dptr(t), nelems, esize, _stream_ptr(stream)), "dev_in_swapn",
+           (T.NC_NOERR,))
+
+
+def dev_swapn(dst, src, nelems, esize, stream=None):
+    _check(lib().pncx_dev_swapn(_dptr(dst), _dptr(src), nelems, esize, _stream_ptr(stream)),
+           "dev_swapn", (T.NC_NOERR,))
+
+
+def dev_putn(cdf_ver, xtype, dx, di, nelems, itype, fillp=None, dstatus=None, stream=None):
+    fb = None if fillp is None else np.frombuffer(bytes(fillp) + b"\0" * 8, np.uint8).copy()
+    _check(lib().pncx_dev_putn(cdf_ver, xtype, _dptr(dx), _dptr(di), nelems, itype,
+                               None if fb is None else _np_ptr(fb),
+                               None if dstatus is None else _dptr(dstatus), _stream_ptr(stream)),
+           "dev_putn", (T.NC_NOERR,))
+
+
+def dev_getn(cdf_ver, xtype, dx, di, nelems, itype, dstatus=None, stream=None):
+    _check(lib().pncx_dev_getn(cdf_ver, xtype, _dptr(dx), _dptr(di), nelems, itype,
+                               None if dstatus is None else _dptr(dstatus), _stream_ptr(stream)),
+           "dev_getn", (T.NC_NOERR,))
+
+
+def dev_batch(segs, stream=None):
+    """Device batch: like ``batch`` but xbuf/ibuf are CUDA tensors."""
+    arr = (Seg * len(segs))()
+    keep = []
+    for k, s in enumerate(segs):
+        fb = None
+        if s.get("fill") is not None:
+            fb = np.frombuffer(bytes(s["fill"]) + b"\0" * 8, np.uint8).copy()
+            keep.append(fb)
+        arr[k] = Seg(s["dir"], s.get("cdf_ver", 5), s["xtype"], s["itype"], s["nelems"],
+                     s["xbuf"].data_ptr(), s["ibuf"].data_ptr(),
+                     None if fb is None else fb.ctypes.data)
+    st = (ctypes.c_int * len(segs))()
+    rc = lib().pncx_dev_batch(arr, len(segs), st, _stream_ptr(stream))
+    if rc not in (T.NC_NOERR, T.NC_ERANGE, T.NC_EBADTYPE, T.NC_ECHAR):
+        raise PncxError(rc, "dev_batch")
+    return list(st)
