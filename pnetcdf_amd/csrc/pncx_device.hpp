@@ -3,8 +3,8 @@
 //
 // One function per direction (get1: external -> internal, put1: internal ->
 // external), specialised at compile time on (xtype, itype).  The rules are
-// those of PnetCDF's ncx.m4 with ERANGE_FILL (see the oracle for the
-// per-macro citations); the float->int casts reproduce what the reference's
+// those of PnetCDF's ncx.m4 with ERANGE_FILL (macros cited per rule below);
+// the float->int casts reproduce what the reference's
 // x86-64 gcc -O2 build does for NaN and for the 2^63 / 2^64 edges, because
 // the GPU conversion instructions differ there (v_cvt_i32_f64(NaN) = 0).
 #pragma once

@@ -153,6 +153,18 @@ static int classify(int dir, int cdf_ver, int xtype, int itype, const void *fill
     return NC_NOERR;
 }
 
+/* nontemporal ("streaming") loads/stores: on by default (every byte is
+ * touched once); PNCX_NONTEMPORAL=-1 selects plain accesses for A/B runs. */
+static int nontemporal_mode(void)
+{
+    static int v = 2;
+    if (v == 2) {
+        const char *e = getenv("PNCX_NONTEMPORAL");
+        v = e ? atoi(e) : 1;
+    }
+    return v;
+}
+
 static int launch_op(const op_t *op, const void *src, void *dst, long long n, int *dstatus,
                      void *stream)
 {
@@ -163,7 +175,7 @@ static int launch_op(const op_t *op, const void *src, void *dst, long long n, in
     a.fill = op->fill;
     a.status = dstatus;
     a.stream = stream;
-    a.nontemporal = 0;
+    a.nontemporal = nontemporal_mode();
     switch (op->kind) {
         case PNCXK_SWAP: return pncxk_swap(op->a, &a);
         case PNCXK_GET: return pncxk_get(op->a, op->b, &a);
@@ -193,10 +205,7 @@ int pncx_dev_swapn(void *ddst, const void *dsrc, pncx_offset nelems, int esize,
     a.dst = ddst;
     a.n = nelems;
     a.stream = stream;
-    {
-        const char *nt = getenv("PNCX_NONTEMPORAL");
-        a.nontemporal = nt ? atoi(nt) : 0;
-    }
+    a.nontemporal = nontemporal_mode();
     return pncxk_swap(esize, &a);
 }
 

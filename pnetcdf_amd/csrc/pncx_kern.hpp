@@ -152,58 +152,38 @@ __device__ __forceinline__ void publish_status(int *status, bool bad) {
         __hip_atomic_store(status, NC_ERANGE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <class Op, int UNROLL, bool NT>
+// XCD-contiguous block order: under the observed round-robin dispatch,
+// blocks b and b+8 share an XCD; remapping gives each XCD one contiguous
+// address range (bijective for any nb; speed only, never correctness --
+// cdna_hip_programming.md §5.5 T1 / "XCD swizzle must be bijective").
+__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nb) {
+    const int64_t q = nb >> 3, r = nb & 7, x = b & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
+// One vector step per lane ("one-shot" grid): measured 6.6 TB/s for the
+// 32 GiB in-place 8-byte swap vs <=5.5 TB/s for grid-stride loops
+// (profiles/ and DESIGN.md).  For grids beyond MAX_BLOCKS the lanes loop.
+constexpr int64_t MAX_BLOCKS = 1LL << 23;
+
+template <class Op, bool NT>
 __global__ __launch_bounds__(256) void k_stream(const uint8_t *src, uint8_t *dst, int64_t head,
                                                 int64_t nvec, int64_t n,
                                                 typename Op::fill_t fill, int *status) {
     constexpr int SB = Op::VEC * Op::SS, DB = Op::VEC * Op::DS;
-    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t nb = gridDim.x;
+    const int64_t tid = xcd_remap(blockIdx.x, nb) * 256 + threadIdx.x;
+    const int64_t stride = nb * 256;
     bool bad = false;
 
-    // scalar head / tail (a few elements)
-    const int64_t tail0 = head + nvec * Op::VEC;
-    if (tid < head) scalar_elem<Op>(src, dst, tid, fill, bad);
-    if (tail0 + tid < n) scalar_elem<Op>(src, dst, tail0 + tid, fill, bad);
-
+    if (blockIdx.x == 0) {  // scalar head / tail (fewer than 16 elements each)
+        const int64_t tail0 = head + nvec * Op::VEC;
+        if (threadIdx.x < head) scalar_elem<Op>(src, dst, threadIdx.x, fill, bad);
+        if (tail0 + threadIdx.x < n) scalar_elem<Op>(src, dst, tail0 + threadIdx.x, fill, bad);
+    }
     const uint8_t *vs = src + head * Op::SS;
     uint8_t *vd = dst + head * Op::DS;
-    int64_t v = tid;
-    for (; v + (UNROLL - 1) * stride < nvec; v += UNROLL * stride) {
-        if constexpr (UNROLL == 1) {
-            vec_step<Op, NT>(vs + v * SB, vd + v * DB, fill, bad);
-        } else {
-            // all loads of the UNROLL steps first, then convert + store
-            constexpr int NS = SB / 16, ND = DB / 16;
-            using SU = typename Op::SU;
-            using DU = typename Op::DU;
-            u32x4 sv[UNROLL][NS];
-#pragma unroll
-            for (int u = 0; u < UNROLL; u++)
-#pragma unroll
-                for (int k = 0; k < NS; k++) sv[u][k] = ld16<NT>(vs + (v + u * stride) * SB + 16 * k);
-            u32x4 ov[UNROLL][ND];
-            if constexpr (Op::PRESERVE) {
-#pragma unroll
-                for (int u = 0; u < UNROLL; u++)
-#pragma unroll
-                    for (int k = 0; k < ND; k++) ov[u][k] = ld16<false>(vd + (v + u * stride) * DB + 16 * k);
-            }
-#pragma unroll
-            for (int u = 0; u < UNROLL; u++) {
-                SU s[Op::VEC];
-                DU d[Op::VEC];
-                __builtin_memcpy(s, sv[u], SB);
-                if constexpr (Op::PRESERVE) __builtin_memcpy(d, ov[u], DB);
-#pragma unroll
-                for (int e = 0; e < Op::VEC; e++) d[e] = Op::one(s[e], d[e], fill, bad);
-                __builtin_memcpy(ov[u], d, DB);
-#pragma unroll
-                for (int k = 0; k < ND; k++) st16<NT>(vd + (v + u * stride) * DB + 16 * k, ov[u][k]);
-            }
-        }
-    }
-    for (; v < nvec; v += stride) vec_step<Op, NT>(vs + v * SB, vd + v * DB, fill, bad);
+    for (int64_t v = tid; v < nvec; v += stride) vec_step<Op, NT>(vs + v * SB, vd + v * DB, fill, bad);
 
     publish_status(status, bad);
 }
@@ -225,7 +205,7 @@ __global__ __launch_bounds__(256) void k_scalar(const uint8_t *src, uint8_t *dst
 // BATCH_STEPS vector steps of it (thread-strided inside the block, so each
 // wave-instruction still moves 1 KiB contiguously).
 // ---------------------------------------------------------------------------
-constexpr int BATCH_STEPS = 8;  // vector steps per lane per block
+constexpr int BATCH_STEPS = 4;  // vector steps per lane per block
 
 template <class Op, bool NT>
 __global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg) {
@@ -289,13 +269,14 @@ int launch_stream(const pncxk_args *a) {
                            (typename Op::fill_t)a->fill, a->status);
     } else {
         const int64_t nvec = (n - h) / Op::VEC;
-        constexpr int U = (Op::VEC * Op::SS + Op::VEC * Op::DS) <= 48 ? 4 : 2;
-        const int grid = launch_grid(nvec > 0 ? nvec : 1, U);
-        if (a->nontemporal)
-            hipLaunchKernelGGL((k_stream<Op, U, true>), dim3(grid), dim3(256), 0, st, src, dst, h,
+        int64_t grid = (nvec + 255) / 256;
+        if (grid < 1) grid = 1;
+        if (grid > MAX_BLOCKS) grid = MAX_BLOCKS;
+        if (a->nontemporal >= 0)
+            hipLaunchKernelGGL((k_stream<Op, true>), dim3((unsigned)grid), dim3(256), 0, st, src, dst, h,
                                nvec, n, (typename Op::fill_t)a->fill, a->status);
         else
-            hipLaunchKernelGGL((k_stream<Op, U, false>), dim3(grid), dim3(256), 0, st, src, dst,
+            hipLaunchKernelGGL((k_stream<Op, false>), dim3((unsigned)grid), dim3(256), 0, st, src, dst,
                                h, nvec, n, (typename Op::fill_t)a->fill, a->status);
     }
     return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
@@ -304,7 +285,7 @@ int launch_stream(const pncxk_args *a) {
 template <class Op>
 int launch_batch(const pncxk_batch_args *a) {
     if (a->nblocks <= 0) return 0;
-    hipLaunchKernelGGL((k_batch<Op, false>), dim3((unsigned)a->nblocks), dim3(256), 0,
+    hipLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0,
                        (hipStream_t)a->stream, a->dsegs, a->nseg);
     return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
 }

@@ -1,0 +1,111 @@
+"""The C-ABI libraries load and export every declared symbol (CPU, no GPU).
+
+No compute call is made here; host-side metadata functions are checked
+against the oracle, and the compute entry points must fail loudly
+(PNCX_EDEVICE) when no GPU is visible instead of silently converting on the
+CPU.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from pnetcdf_amd import nctypes as T
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "pnetcdf_amd", "lib", "libpncx.so")
+LIB_MPI = os.path.join(ROOT, "pnetcdf_amd", "lib", "libpncx_ncmpii.so")
+
+
+def declared(header):
+    src = open(os.path.join(ROOT, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_]+\s*\*?\s*(\w+)\s*\(", src, flags=re.M)
+    return sorted(set(n for n in names if n.startswith(("pncx_", "ncmpii_"))))
+
+
+def exported(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True,
+                         check=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+
+
+@pytest.fixture(scope="module")
+def built():
+    if not os.path.exists(LIB) or not os.path.exists(LIB_MPI):
+        subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "pnetcdf_amd", "csrc")], check=True)
+    return True
+
+
+def test_pncx_h_symbols_exported(built):
+    decl = declared("pncx.h")
+    assert len(decl) == 19
+    missing = [s for s in decl if s not in exported(LIB)]
+    assert not missing, missing
+
+
+def test_ncmpii_symbols_exported(built):
+    decl = declared("pncx_ncmpii.h")
+    # the 22 conversion symbols of common.h:147-221 (+ CHAR put/get, mapper)
+    assert {"ncmpii_in_swapn", "ncmpii_need_convert", "ncmpii_putn_NC_DOUBLE",
+            "ncmpii_getn_NC_INT", "ncmpii_putn_NC_BYTE", "ncmpii_getn_NC_UINT64"} <= set(decl)
+    assert len([d for d in decl if d.startswith("ncmpii_")]) == 24
+    missing = [s for s in decl if s not in exported(LIB_MPI)]
+    assert not missing, missing
+
+
+def test_library_loads_and_metadata(built):
+    from oracle import oracle as O
+    L = ctypes.CDLL(LIB)
+    L.pncx_version.restype = ctypes.c_char_p
+    assert b"gfx950" in L.pncx_version()
+    for fmt in (1, 2, 5):
+        for xt in T.NUMERIC_XTYPES + [T.NC_CHAR]:
+            for it in T.NUMERIC_ITYPES + [T.ITYPE_CHAR]:
+                assert L.pncx_need_convert(fmt, xt, it) == O.need_convert(fmt, xt, it)
+    for xt in T.NUMERIC_XTYPES:
+        assert L.pncx_xlen(xt) == T.xlen(xt)
+        for it in T.NUMERIC_ITYPES:
+            assert L.pncx_need_swap(xt, it) == O.need_swap(xt, it)
+    for it in T.NUMERIC_ITYPES:
+        assert L.pncx_ilen(it) == T.ilen(it)
+    assert L.pncx_xlen(99) == -1 and L.pncx_ilen(99) == -1
+
+
+def test_no_cpu_fallback_without_gpu(built):
+    """With no visible GPU the host entry points return PNCX_EDEVICE."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible: covered by the gpu tests")
+    L = ctypes.CDLL(LIB)
+    assert L.pncx_device_count() == 0
+    buf = np.arange(16, dtype=np.int64)
+    keep = buf.copy()
+    rc = L.pncx_in_swapn(ctypes.c_void_p(buf.ctypes.data), ctypes.c_longlong(16), 8)
+    assert rc == T.PNCX_EDEVICE
+    assert np.array_equal(buf, keep)            # untouched: no silent CPU path
+    xb = np.zeros(128, np.uint8)
+    rc = L.pncx_putn(5, T.NC_INT, ctypes.c_void_p(xb.ctypes.data), ctypes.c_void_p(buf.ctypes.data),
+                     ctypes.c_longlong(16), T.ITYPE_LONGLONG, None)
+    assert rc == T.PNCX_EDEVICE
+    # argument errors are still reported before the device check
+    rc = L.pncx_putn(5, 42, ctypes.c_void_p(xb.ctypes.data), ctypes.c_void_p(buf.ctypes.data),
+                     ctypes.c_longlong(16), T.ITYPE_INT, None)
+    assert rc == T.NC_EBADTYPE
+
+
+def test_product_does_not_reference_oracle():
+    """The product sources never include, link or load the oracle."""
+    for d, _, files in os.walk(os.path.join(ROOT, "pnetcdf_amd")):
+        for f in files:
+            if f.endswith((".c", ".h", ".hpp", ".hip", ".py", "Makefile")):
+                txt = open(os.path.join(d, f)).read()
+                for pat in ("import oracle", "from oracle", "liboracle", "orc_", "pncx_oracle"):
+                    assert pat not in txt, (os.path.join(d, f), pat)
+    for lib in (LIB, LIB_MPI):
+        if os.path.exists(lib):
+            out = subprocess.run(["readelf", "-d", lib], capture_output=True, text=True).stdout
+            assert "oracle" not in out

@@ -1,0 +1,340 @@
+"""Parity of the HIP path against the CPU oracle and the golden fixtures (GPU).
+
+Bar: bit-exact outputs and identical status for every (xtype, itype) pair,
+both directions, through the C-ABI (host-buffer and device-buffer entry
+points).  Cross-type float casts are also bit-exact here (stricter than the
+north star's 1-ulp allowance): tolerance = 0 ulp.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from pnetcdf_amd import nctypes as T
+from tests import reftests
+from tests.converters import HipDevConv, HipHostConv, OracleConv
+
+pytestmark = pytest.mark.gpu
+
+GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "edge_vectors.npz"))
+
+
+def pairs():
+    for xt in T.NUMERIC_XTYPES:
+        for it in T.NUMERIC_ITYPES:
+            k = f"{T.XNAME[xt]}_{T.INAME[it]}"
+            yield 5, xt, it, k
+            if xt == T.NC_BYTE and it == T.ITYPE_UCHAR:
+                yield 2, xt, it, k + "_cdf2"
+
+
+PAIRS = list(pairs())
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU test run without a visible GPU"
+    from pnetcdf_amd import pncx
+    assert pncx.device_count() >= 1
+    return torch
+
+
+@pytest.fixture(scope="module", params=["host", "dev"])
+def conv(request, torch_cuda):
+    return HipHostConv() if request.param == "host" else HipDevConv()
+
+
+# ------------------------------------------------------------------ golden
+@pytest.mark.parametrize("cdf,xt,it,k", PAIRS, ids=[p[3] for p in PAIRS])
+def test_golden_edges(conv, cdf, xt, it, k):
+    res, st = conv.getn(cdf, xt, GOLD[f"get_{k}_in"].tobytes(), it)
+    assert st == GOLD[f"get_{k}_st"][0]
+    exp = GOLD[f"get_{k}_out"].tobytes()
+    got = res.tobytes()
+    if got != exp:
+        e = np.frombuffer(exp, T.ITYPE_NP[it])
+        bad = np.nonzero(res.view(np.uint8).reshape(res.size, -1).tobytes() != exp)[0]
+        idx = [i for i in range(res.size) if res[i:i + 1].tobytes() != e[i:i + 1].tobytes()][:5]
+        xin = np.frombuffer(GOLD[f"get_{k}_in"].tobytes(), T.XTYPE_BE[xt])
+        pytest.fail(f"get mismatch at {idx}: in {[xin[i] for i in idx]} got {[res[i] for i in idx]} "
+                    f"exp {[e[i] for i in idx]} ({len(bad)})")
+    iin = np.frombuffer(GOLD[f"put_{k}_in"].tobytes(), T.ITYPE_NP[it])
+    for tag, fill in (("dflt", T.fill_bytes(xt)), ("user", T.fill_bytes(xt, 99)), ("null", None)):
+        xb, st = conv.putn(cdf, xt, iin, it, fill, xinit=GOLD[f"put_{k}_xinit"].tobytes())
+        assert st == GOLD[f"put_{k}_{tag}_st"][0], tag
+        exp = GOLD[f"put_{k}_{tag}_out"].tobytes()
+        if xb != exp:
+            xs = T.xlen(xt)
+            idx = [i for i in range(iin.size) if xb[i * xs:(i + 1) * xs] != exp[i * xs:(i + 1) * xs]][:5]
+            pytest.fail(f"put {tag} mismatch at {idx}: in {[iin[i] for i in idx]} got "
+                        f"{[xb[i*xs:(i+1)*xs].hex() for i in idx]} exp {[exp[i*xs:(i+1)*xs].hex() for i in idx]}")
+
+
+# ------------------------------------------------- random bits vs the oracle
+@pytest.mark.parametrize("xt", T.NUMERIC_XTYPES, ids=[T.XNAME[x] for x in T.NUMERIC_XTYPES])
+def test_random_bits_vs_oracle(conv, xt):
+    ora = OracleConv()
+    rng = np.random.default_rng(0x5EED0000 + xt)
+    for it in T.NUMERIC_ITYPES:
+        for n in (1, 7, 33, 4099):
+            raw = rng.integers(0, 256, n * 8, dtype=np.uint8)
+            ib = np.frombuffer(raw.tobytes(), T.ITYPE_NP[it])[:n].copy()
+            fill = T.fill_bytes(xt, 77)
+            assert conv.putn(5, xt, ib, it, fill) == ora.putn(5, xt, ib, it, fill), (T.INAME[it], n)
+            xr = rng.integers(0, 256, n * T.xlen(xt), dtype=np.uint8).tobytes()
+            g, sg = conv.getn(5, xt, xr, it)
+            o, so = ora.getn(5, xt, xr, it)
+            assert sg == so and g.tobytes() == o.tobytes(), (T.INAME[it], n)
+
+
+# ------------------------------------- the reference's own test expectations
+@pytest.mark.parametrize("cdf", [2, 5])
+def test_reference_nc_test(conv, cdf):
+    fails = []
+    for xt in T.NUMERIC_XTYPES:
+        if cdf < 5 and xt in (T.NC_UBYTE, T.NC_USHORT, T.NC_UINT, T.NC_INT64, T.NC_UINT64):
+            continue
+        for it in T.NUMERIC_ITYPES:
+            fails += [f"{T.XNAME[xt]}/{T.INAME[it]}: {m}" for m in reftests.nc_test_put_get(conv, cdf, xt, it)]
+    assert not fails, "\n".join(fails[:20])
+
+
+def test_reference_test_erange(conv):
+    fails = reftests.test_erange_cases(conv)
+    assert not fails, "\n".join(fails)
+
+
+@pytest.mark.parametrize("cdf", [2, 5])
+def test_reference_erange_fill(conv, cdf):
+    fails = reftests.erange_fill_cases(conv, cdf)
+    assert not fails, "\n".join(fails)
+
+
+# ------------------------------------------------------------------- swaps
+@pytest.mark.parametrize("esize", [2, 3, 4, 8, 16])
+@pytest.mark.parametrize("n", [0, 1, 15, 17, 1000, 100003])
+def test_host_in_swapn(torch_cuda, esize, n):
+    from oracle import oracle as O
+    from pnetcdf_amd import pncx
+    rng = np.random.default_rng(esize * 1000 + n)
+    buf = rng.integers(0, 256, n * esize, dtype=np.uint8)
+    ref = buf.copy()
+    O.in_swapn(ref, esize)
+    pncx.in_swapn(buf, n, esize)
+    assert np.array_equal(buf, ref)
+
+
+@pytest.mark.parametrize("esize", [2, 4, 8])
+@pytest.mark.parametrize("offset", [0, 1, 2, 4, 8, 12])
+def test_dev_swap_offsets(torch_cuda, esize, offset):
+    """Element-aligned and misaligned device slabs (head/tail/scalar paths)."""
+    torch = torch_cuda
+    from oracle import oracle as O
+    from pnetcdf_amd import pncx
+    n = 4096 + 5
+    rng = np.random.default_rng(offset)
+    raw = rng.integers(0, 256, n * esize + 64, dtype=np.uint8)
+    d = torch.from_numpy(raw.copy()).cuda()
+    view = d[offset:offset + n * esize]
+    lib = pncx.lib()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert lib.pncx_dev_in_swapn(ctypes.c_void_p(view.data_ptr()), n, esize, stream) == 0
+    torch.cuda.synchronize()
+    ref = raw.copy()
+    seg = ref[offset:offset + n * esize]
+    O.in_swapn(seg, esize)
+    assert np.array_equal(d.cpu().numpy(), ref)
+
+
+def test_dev_swapn_out_of_place(torch_cuda):
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    n = 1 << 20
+    a = torch.randint(-2**62, 2**62, (n,), dtype=torch.int64, device="cuda")
+    b = torch.empty_like(a)
+    pncx.dev_swapn(b, a, n, 8)
+    torch.cuda.synchronize()
+    assert torch.equal(b.view(torch.uint8).view(-1, 8).flip(1).reshape(-1), a.view(torch.uint8))
+
+
+def test_misaligned_conversion(torch_cuda):
+    """Pointers that cannot be co-aligned to 16 B take the scalar kernel."""
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    ora = OracleConv()
+    lib = pncx.lib()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    n = 1000
+    rng = np.random.default_rng(3)
+    xr = rng.integers(0, 256, 4 * n, dtype=np.uint8)
+    dx = torch.zeros(4 * n + 64, dtype=torch.uint8, device="cuda")
+    dx[1:1 + 4 * n] = torch.from_numpy(xr).cuda()
+    di = torch.zeros(8 * n + 64, dtype=torch.uint8, device="cuda")
+    ds = torch.zeros(1, dtype=torch.int32, device="cuda")
+    rc = lib.pncx_dev_getn(5, T.NC_INT, ctypes.c_void_p(dx.data_ptr() + 1), ctypes.c_void_p(di.data_ptr() + 3),
+                           n, T.ITYPE_DOUBLE, ctypes.c_void_p(ds.data_ptr()), stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    o, so = ora.getn(5, T.NC_INT, xr.tobytes(), T.ITYPE_DOUBLE)
+    assert di.cpu().numpy()[3:3 + 8 * n].tobytes() == o.tobytes() and int(ds.item()) == so
+
+
+def test_errors(torch_cuda):
+    from pnetcdf_amd import pncx
+    lib = pncx.lib()
+    x = np.zeros(64, np.uint8)
+    assert lib.pncx_putn(5, 99, x.ctypes.data, x.ctypes.data, 4, T.ITYPE_INT, None) == T.NC_EBADTYPE
+    assert lib.pncx_putn(5, T.NC_INT, x.ctypes.data, x.ctypes.data, 4, 77, None) == T.NC_EBADTYPE
+    assert lib.pncx_putn(5, T.NC_CHAR, x.ctypes.data, x.ctypes.data, 4, T.ITYPE_INT, None) == T.NC_ECHAR
+    assert lib.pncx_getn(5, T.NC_INT, x.ctypes.data, x.ctypes.data, 4, T.ITYPE_CHAR) == T.NC_ECHAR
+    assert lib.pncx_getn(5, T.NC_INT, x.ctypes.data, x.ctypes.data, 0, T.ITYPE_INT) == T.NC_NOERR
+    # NC_CHAR <-> char is a copy
+    src = np.frombuffer(b"hello, netcdf!!!", np.uint8).copy()
+    dst = np.zeros(16, np.uint8)
+    assert lib.pncx_getn(5, T.NC_CHAR, src.ctypes.data, dst.ctypes.data, 16, T.ITYPE_CHAR) == 0
+    assert dst.tobytes() == b"hello, netcdf!!!"
+
+
+def test_put_leaves_user_buffer_intact(torch_cuda):
+    """test_erange.c:199,217: the caller's put buffer is never altered."""
+    from pnetcdf_amd import pncx
+    ib = np.array([-129, 256, 5, 70000] * 1000, np.int32)
+    keep = ib.copy()
+    xb = np.zeros(ib.size, np.uint8)
+    st = pncx.putn(5, T.NC_BYTE, xb, ib, ib.size, T.ITYPE_INT, T.fill_bytes(T.NC_BYTE))
+    assert st == T.NC_ERANGE and np.array_equal(ib, keep)
+
+
+# ------------------------------------------------------------------- batch
+def _c4_segments(rng, nvar=256, nel=1 << 14, mixed_cast=False):
+    segs = []
+    for v in range(nvar):
+        if v % 2 == 0:
+            xt, it = T.NC_SHORT, (T.ITYPE_FLOAT if mixed_cast else T.ITYPE_SHORT)
+            if mixed_cast:
+                ib = rng.uniform(-40000, 40000, nel).astype(np.float32)
+            else:
+                ib = rng.integers(-32768, 32767, nel, dtype=np.int16)
+        else:
+            xt, it = T.NC_FLOAT, T.ITYPE_FLOAT
+            ib = rng.standard_normal(nel).astype(np.float32)
+        segs.append(dict(dir=T.PNCX_PUT, cdf_ver=5, xtype=xt, itype=it, nelems=nel,
+                         xbuf=np.zeros(nel * T.xlen(xt), np.uint8), ibuf=ib, fill=T.fill_bytes(xt)))
+    return segs
+
+
+@pytest.mark.parametrize("mixed_cast", [False, True])
+def test_host_batch_c4(torch_cuda, mixed_cast):
+    from pnetcdf_amd import pncx
+    ora = OracleConv()
+    rng = np.random.default_rng(0x5EED0004)
+    segs = _c4_segments(rng, mixed_cast=mixed_cast)
+    st = pncx.batch(segs)
+    for s, stv in zip(segs, st):
+        xb, so = ora.putn(5, s["xtype"], s["ibuf"], s["itype"], s["fill"])
+        assert stv == so and s["xbuf"].tobytes() == xb
+
+
+def test_dev_batch_mixed_classes(torch_cuda):
+    """Segments of many classes, sizes and alignments in one call."""
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    ora = OracleConv()
+    rng = np.random.default_rng(11)
+    segs, refs = [], []
+    combos = [(T.PNCX_GET, T.NC_INT, T.ITYPE_DOUBLE), (T.PNCX_PUT, T.NC_SHORT, T.ITYPE_FLOAT),
+              (T.PNCX_GET, T.NC_DOUBLE, T.ITYPE_DOUBLE), (T.PNCX_PUT, T.NC_BYTE, T.ITYPE_INT),
+              (T.PNCX_GET, T.NC_UINT64, T.ITYPE_FLOAT), (T.PNCX_PUT, T.NC_USHORT, T.ITYPE_SCHAR),
+              (T.PNCX_GET, T.NC_SHORT, T.ITYPE_SHORT), (T.PNCX_PUT, T.NC_FLOAT, T.ITYPE_FLOAT)]
+    for k in range(40):
+        d, xt, it = combos[k % len(combos)]
+        n = int(rng.integers(0, 20000))
+        raw = rng.integers(0, 256, n * 8 + 8, dtype=np.uint8)
+        if d == T.PNCX_GET:
+            xin = raw[: n * T.xlen(xt)].tobytes()
+            exp, so = ora.getn(5, xt, xin, it)
+            dx = torch.from_numpy(np.frombuffer(xin + b"\0" * 16, np.uint8).copy()).cuda()
+            di = torch.zeros(n * T.ilen(it) + 16, dtype=torch.uint8, device="cuda")
+            refs.append((di, exp.tobytes(), so, n * T.ilen(it)))
+        else:
+            ib = np.frombuffer(raw.tobytes(), T.ITYPE_NP[it])[:n].copy()
+            xb, so = ora.putn(5, xt, ib, it, T.fill_bytes(xt))
+            di = torch.from_numpy(np.frombuffer(ib.tobytes() + b"\0" * 16, np.uint8).copy()).cuda()
+            dx = torch.zeros(n * T.xlen(xt) + 16, dtype=torch.uint8, device="cuda")
+            refs.append((dx, xb, so, n * T.xlen(xt)))
+        segs.append(dict(dir=d, cdf_ver=5, xtype=xt, itype=it, nelems=n, xbuf=dx, ibuf=di,
+                         fill=T.fill_bytes(xt) if d == T.PNCX_PUT else None))
+    st = pncx.dev_batch(segs)
+    torch.cuda.synchronize()
+    for (buf, exp, so, nb), stv in zip(refs, st):
+        assert stv == so
+        assert buf.cpu().numpy()[:nb].tobytes() == exp
+
+
+# ------------------------------------------- full-size (BASELINE) properties
+def _splitmix64_torch(torch, n, seed, chunk=1 << 27):
+    """splitmix64 stream on the GPU (element i = mix(seed + (i+1)*golden)),
+    generated in chunks to bound temporaries; int64 arithmetic wraps."""
+    out = torch.empty(n, dtype=torch.int64, device="cuda")
+    for s in range(0, n, chunk):
+        m = min(chunk, n - s)
+        z = torch.arange(s + 1, s + 1 + m, dtype=torch.int64, device="cuda")
+        z.mul_(-7046029254386353131).add_(seed)                    # 0x9E3779B97F4A7C15
+        z = (z ^ ((z >> 30) & 0x3FFFFFFFF)) * -4658895280553007687  # 0xBF58476D1CE4E5B9
+        z = (z ^ ((z >> 27) & 0x1FFFFFFFFF)) * -7723592293110705685 # 0x94D049BB133111EB
+        out[s:s + m] = z ^ ((z >> 31) & 0x1FFFFFFFF)
+    return out
+
+
+def _splitmix64_np(idx, seed):
+    z = (idx.astype(np.uint64) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(seed)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return (z ^ (z >> np.uint64(31))).view(np.int64)
+
+
+@pytest.mark.slow
+def test_c2_full_size_swap_properties(torch_cuda):
+    """Config 2 at its BASELINE size (32 GiB NC_DOUBLE): one in-place swap
+    equals torch's byte reversal on sampled windows, and swapping twice is
+    the identity (checksum), sampled elements vs the oracle."""
+    torch = torch_cuda
+    from oracle import oracle as O
+    from pnetcdf_amd import pncx
+    n = (32 << 30) // 8
+    x = _splitmix64_torch(torch, n, 0x5EED0002)
+    chk0 = int(x[::4099].sum().item())
+    pncx.dev_in_swapn(x, n, 8)
+    torch.cuda.synchronize()
+    idx = torch.randint(0, n, (4096,), device="cuda")
+    idx[:4] = torch.tensor([0, 1, n - 2, n - 1], device="cuda")
+    orig = _splitmix64_np(idx.cpu().numpy(), 0x5EED0002)
+    ref = orig.copy()
+    O.in_swapn(ref, 8)
+    assert np.array_equal(x[idx].cpu().numpy(), ref)
+    pncx.dev_in_swapn(x, n, 8)
+    torch.cuda.synchronize()
+    assert int(x[::4099].sum().item()) == chk0
+    del x
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.slow
+def test_c3_full_size_int_to_double(torch_cuda):
+    """Config 3: 2^31 NC_INT (big-endian) -> double; every element equals
+    the byte-reversed int32 as float64 (torch computes the reference)."""
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    n = 1 << 31
+    xr = _splitmix64_torch(torch, n // 2, 0x5EED0003).view(torch.int32)
+    dst = torch.empty(n, dtype=torch.float64, device="cuda")
+    ds = torch.zeros(1, dtype=torch.int32, device="cuda")
+    pncx.dev_getn(5, T.NC_INT, xr, dst, n, T.ITYPE_DOUBLE, ds)
+    torch.cuda.synchronize()
+    assert int(ds.item()) == 0
+    step = 1 << 26
+    for s in range(0, n, step):
+        native = xr[s:s + step].view(torch.uint8).view(-1, 4).flip(1).reshape(-1).view(torch.int32)
+        assert torch.equal(dst[s:s + step], native.to(torch.float64))

@@ -1,0 +1,163 @@
+"""Pin the CPU oracle to the reference (CPU, no GPU).
+
+The reference's conversion code cannot be built in this image (m4 sources,
+no GNU m4 / configure; DESIGN.md "Oracle"), so the oracle is pinned by:
+  1. known answers recorded from the compiled reference,
+  2. the reference test suite's own expectations, restated in reftests.py
+     (nc_test hash/inRange3/equal, test_erange.c, erange_fill.m4),
+  3. the reference-held data file src/utils/ncmpidiff/tst_file.nc.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from pnetcdf_amd import nctypes as T
+from tests import reftests
+from tests.converters import OracleConv
+from tests.cdfparse import parse_cdf
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _val(v):
+    return float("nan") if v == "nan" else v
+
+
+def load_known():
+    with open(os.path.join(GOLD, "known_answers.json")) as f:
+        return json.load(f)
+
+
+KNOWN = load_known()
+
+
+@pytest.mark.parametrize("case", KNOWN["cases"], ids=[c["id"] for c in KNOWN["cases"]])
+def test_known_answers(oracle, case):
+    xt, it = T.XTYPES[case["xtype"]], T.ITYPES[case["itype"]]
+    if case["dir"] == "get":
+        if "x_hex" in case:
+            xb = bytes.fromhex(case["x_hex"])
+        else:
+            xb = np.array([_val(v) for v in case["x_values"]], dtype=T.XTYPE_BE[xt]).tobytes()
+        out, st = oracle.getn(case["cdf"], xt, xb, it)
+        assert st == case["status"]
+        if "expect" in case:
+            assert [int(v) if np.issubdtype(out.dtype, np.integer) else float(v) for v in out] == case["expect"]
+        else:
+            nb = out.dtype.itemsize
+            got = [int.from_bytes(out[k:k + 1].tobytes(), "little") for k in range(out.size)]
+            assert got == [int(h, 16) & ((1 << (8 * nb)) - 1) for h in case["expect_u64"]]
+    else:
+        ib = np.array([_val(v) for v in case["input"]], dtype=T.ITYPE_NP[it])
+        xb, st = oracle.putn(case["cdf"], xt, ib, it, fill=T.fill_bytes(xt))
+        assert st == case["status"]
+        assert xb.hex() == case["x_hex"]
+
+
+@pytest.mark.parametrize("c", KNOWN["need_convert"])
+def test_known_need_convert(oracle, c):
+    assert oracle.need_convert(c["fmt"], T.XTYPES[c["xtype"]], T.ITYPES[c["itype"]]) == c["expect"]
+
+
+def test_need_convert_matrix(oracle):
+    # convert_swap.m4:85-116 for every pair and format, vs the Python restatement
+    for fmt in (1, 2, 5):
+        for xt in T.NUMERIC_XTYPES:
+            for it in T.NUMERIC_ITYPES:
+                assert oracle.need_convert(fmt, xt, it) == T.need_convert(fmt, xt, it)
+    assert oracle.need_convert(5, T.NC_CHAR, T.ITYPE_CHAR) == 0
+    assert oracle.need_swap(T.NC_BYTE, T.ITYPE_SCHAR) == 0
+    assert oracle.need_swap(T.NC_UBYTE, T.ITYPE_UCHAR) == 0
+    assert oracle.need_swap(T.NC_CHAR, T.ITYPE_CHAR) == 0
+    assert oracle.need_swap(T.NC_SHORT, T.ITYPE_SHORT) == 1
+
+
+@pytest.mark.parametrize("cdf", [2, 5])
+@pytest.mark.parametrize("xtype", T.NUMERIC_XTYPES, ids=[T.XNAME[x] for x in T.NUMERIC_XTYPES])
+def test_nc_test_expectations(cdf, xtype):
+    conv = OracleConv()
+    fails = []
+    for it in T.NUMERIC_ITYPES:
+        if cdf < 5 and xtype in (T.NC_UBYTE, T.NC_USHORT, T.NC_UINT, T.NC_INT64, T.NC_UINT64):
+            continue  # CDF-5 only types
+        fails += [f"{T.INAME[it]}: {m}" for m in reftests.nc_test_put_get(conv, cdf, xtype, it)]
+    assert not fails, "\n".join(fails)
+
+
+def test_test_erange():
+    fails = reftests.test_erange_cases(OracleConv())
+    assert not fails, "\n".join(fails)
+
+
+@pytest.mark.parametrize("cdf", [2, 5])
+def test_erange_fill(cdf):
+    fails = reftests.erange_fill_cases(OracleConv(), cdf)
+    assert not fails, "\n".join(fails)
+
+
+def test_in_swapn_semantics(oracle):
+    # convert_swap.m4:137-197: esize 2/4/8 and the generic n-byte branch,
+    # no-op for esize <= 1 or nelems <= 0
+    rng = np.random.default_rng(0)
+    for es in (1, 2, 3, 4, 5, 8, 16):
+        b = rng.integers(0, 256, es * 37, dtype=np.uint8)
+        ref = b.reshape(-1, es)[:, ::-1].reshape(-1).copy() if es > 1 else b.copy()
+        got = b.copy()
+        oracle.in_swapn(got, es)
+        assert np.array_equal(got, ref), es
+
+
+def test_tst_file_nc_decodes(oracle):
+    """src/utils/ncmpidiff/tst_file.nc (CDF-1, written by the reference):
+    every variable's big-endian payload decodes identically through the
+    oracle's getn and an independent numpy '>' decode, and NC_FLOAT ->
+    int/short conversions follow GETF_CheckBND (ncx.m4:503-513)."""
+    with open(os.path.join(GOLD, "tst_file.nc"), "rb") as f:
+        data = f.read()
+    hdr = parse_cdf(data)
+    assert hdr["version"] == 1
+    checked = 0
+    for v in hdr["vars"]:
+        xt = v["xtype"]
+        for off, n in v["extents"]:
+            raw = data[off:off + n * T.xlen(xt)]
+            if len(raw) < n * T.xlen(xt):
+                continue
+            ref = np.frombuffer(raw, dtype=T.XTYPE_BE[xt]).astype(T.XTYPE_NP[xt])
+            it = {T.NC_FLOAT: T.ITYPE_FLOAT, T.NC_INT: T.ITYPE_INT, T.NC_DOUBLE: T.ITYPE_DOUBLE,
+                  T.NC_SHORT: T.ITYPE_SHORT}[xt]
+            out, st = oracle.getn(1, xt, raw, it)
+            assert st == 0 and np.array_equal(out.view(np.uint8), ref.view(np.uint8))
+            if xt == T.NC_FLOAT:
+                i32, st = oracle.getn(1, xt, raw, T.ITYPE_INT)
+                assert st == 0 and np.array_equal(i32, np.trunc(ref).astype(np.int32))
+            checked += n
+    assert checked > 0
+    # the file's float data: 1,1,1,2,2,2,3,3,3,... and fill-like -999/-888
+    fv = [v for v in hdr["vars"] if v["name"] == "fix_var"][0]
+    off, n = fv["extents"][0]
+    vals = np.frombuffer(data[off:off + 4 * n], ">f4")
+    assert set(np.unique(vals)).issubset({0.0, 1.0, 2.0, 3.0, -999.0, 100.0, 101.0, 102.0, 103.0,
+                                          200.0, 201.0, 202.0, 203.0, -888.0})
+
+
+def test_fill_defaults(oracle):
+    # put of an out-of-range value with fillp == NULL writes FillDefaultValue
+    # of the xtype for the multi-byte codecs (ncx.m4:610,642)
+    for xt, it, v in [(T.NC_SHORT, T.ITYPE_INT, 70000), (T.NC_INT, T.ITYPE_DOUBLE, 1e20),
+                      (T.NC_FLOAT, T.ITYPE_DOUBLE, 1e300), (T.NC_UINT64, T.ITYPE_LONGLONG, -5)]:
+        xb, st = oracle.putn(5, xt, np.array([v], T.ITYPE_NP[it]), it, fill=None)
+        assert st == T.NC_ERANGE
+        assert np.frombuffer(xb, T.XTYPE_BE[xt])[0] == np.array([T.XTYPE_FILL[xt]], T.XTYPE_NP[xt])[0]
+    # 1-byte externals leave the byte untouched (FillValue no-op) ...
+    xb, st = oracle.putn(5, T.NC_BYTE, np.array([1000, 5], np.int32), T.ITYPE_INT, fill=None,
+                         xinit=b"\x7a\x00")
+    assert st == T.NC_ERANGE and xb == b"\x7a\x05"
+    # ... and ushort <- schar swaps the bytes already there (ncx.m4:818-841)
+    xb, st = oracle.putn(5, T.NC_USHORT, np.array([-1], np.int8), T.ITYPE_SCHAR, fill=None,
+                         xinit=b"\x12\x34")
+    assert st == T.NC_ERANGE and xb == b"\x34\x12"
+    assert not math.isnan(0.0)
