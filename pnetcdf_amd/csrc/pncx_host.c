@@ -265,6 +265,8 @@ typedef struct ctx_t {
     int   *dstatus;           /* device status words [NSLOT]   */
     void  *dscratch;          /* batch descriptors / statuses  */
     size_t dscratch_size;
+    void  *hscratch;          /* pinned host mirror of dscratch */
+    size_t hscratch_size;
     pthread_mutex_t lock;
 } ctx_t;
 
@@ -324,13 +326,16 @@ static int ensure_dbuf(ctx_t *c, size_t need)
 
 static int ensure_scratch(ctx_t *c, size_t need)
 {
-    if (c->dscratch_size >= need) return 0;
+    if (c->dscratch_size >= need && c->hscratch_size >= need) return 0;
+    need = need < 65536 ? 65536 : need * 2;
     pncxrt_stream_sync(c->stream[0]);
     pncxrt_free(c->dscratch);
-    c->dscratch = NULL;
-    c->dscratch_size = 0;
+    pncxrt_host_free(c->hscratch);
+    c->dscratch = c->hscratch = NULL;
+    c->dscratch_size = c->hscratch_size = 0;
     if (pncxrt_malloc(&c->dscratch, need) != 0) return PNCX_EDEVICE;
-    c->dscratch_size = need;
+    if (pncxrt_host_alloc(&c->hscratch, need) != 0) return PNCX_EDEVICE;
+    c->dscratch_size = c->hscratch_size = need;
     return 0;
 }
 
@@ -456,47 +461,39 @@ static long long seg_head(const void *src, const void *dst, int ss, int ds, long
     return -1;
 }
 
-/* Launch all items (device buffers) grouped by class, statuses into
- * dstat[idx] (device ints, zeroed by the caller). */
-static int batch_launch(bitem_t *it, int nit, int *dstat, pncxk_seg *dseg, void *stream)
+/* Launch all items (device buffers) grouped by class; statuses go to
+ * dstat[idx] (device ints, zeroed by the caller).  All tile descriptors are
+ * planned first into the pinned mirror hseg, copied to the device in ONE
+ * async copy, then every class is launched back to back on `stream`. */
+typedef struct cls_t { int first, count; long long nblocks; const op_t *op; } cls_t;
+
+static int batch_launch(bitem_t *it, int nit, int *dstat, pncxk_seg *dseg, pncxk_seg *hseg,
+                        void *stream)
 {
-    int i = 0, err = 0;
-    pncxk_seg *hseg = NULL;
+    int i = 0, err = 0, ns = 0, nc = 0, k;
+    cls_t *cls = (cls_t *)malloc(sizeof(cls_t) * (size_t)(nit > 0 ? nit : 1));
+    if (cls == NULL) return NC_ENOMEM;
     qsort(it, (size_t)nit, sizeof *it, cmp_item);
-    hseg = (pncxk_seg *)malloc(sizeof(pncxk_seg) * (size_t)(nit > 0 ? nit : 1));
-    if (hseg == NULL) return NC_ENOMEM;
+    /* pass 1: launch what cannot be batched, plan the rest */
     while (!err && i < nit) {
-        int j = i, ns = 0;
-        long long nblocks = 0;
+        int j = i;
         pncxk_opinfo oi;
         const op_t *op = &it[i].op;
         while (j < nit && it[j].op.kind == op->kind && it[j].op.a == op->a &&
                it[j].op.b == op->b && it[j].op.c == op->c)
             j++;
-        if (op->kind == PNCXK_SWAP && op->a == 1) {          /* 1-byte copies */
-            int k;
+        if (op->kind == PNCXK_SWAP && op->a == 1) {            /* 1-byte copies */
             for (k = i; k < j && !err; k++)
-                if (it[k].dst != it[k].src)
+                if (it[k].dst != it[k].src && it[k].n > 0)
                     err = pncxrt_memcpy_d2d(it[k].dst, it[k].src, (size_t)it[k].n, stream);
-            i = j;
-            continue;
-        }
-        if (op->kind == PNCXK_SWAP && op->a != 2 && op->a != 4 && op->a != 8) {
-            int k;
-            for (k = i; k < j && !err; k++) {
-                pncxk_args a;
-                memset(&a, 0, sizeof a);
-                a.src = it[k].src; a.dst = it[k].dst; a.n = it[k].n; a.stream = stream;
-                err = pncxk_swap_generic(op->a, &a);
-            }
-            i = j;
-            continue;
-        }
-        err = pncxk_opinfo_get(op->kind, op->a, op->b, op->c, &oi);
-        if (err) break;
-        {
-            int k;
-            const long long per_block = (long long)oi.batch_steps * 256;
+        } else if ((op->kind == PNCXK_SWAP && op->a != 2 && op->a != 4 && op->a != 8) || op->c) {
+            /* generic n-byte swaps and NULL-fill (PRESERVE) codecs: one launch each */
+            for (k = i; k < j && !err; k++)
+                err = launch_op(&it[k].op, it[k].src, it[k].dst, it[k].n, dstat + it[k].idx, stream);
+        } else if ((err = pncxk_opinfo_get(op->kind, op->a, op->b, op->c, &oi)) == 0) {
+            cls[nc].first = ns;
+            cls[nc].nblocks = 0;
+            cls[nc].op = op;
             for (k = i; k < j && !err; k++) {
                 const long long h = seg_head(it[k].src, it[k].dst, oi.ss, oi.ds, it[k].n);
                 if (it[k].n <= 0) continue;
@@ -508,32 +505,30 @@ static int batch_launch(bitem_t *it, int nit, int *dstat, pncxk_seg *dseg, void 
                 hseg[ns].dst = it[k].dst;
                 hseg[ns].n = it[k].n;
                 hseg[ns].head = h;
-                hseg[ns].nvec = (it[k].n - h) / oi.vec;
-                hseg[ns].block0 = nblocks;
+                hseg[ns].nvec = (it[k].n - h) / oi.vec;     /* full block tiles */
+                hseg[ns].block0 = cls[nc].nblocks;
                 hseg[ns].fill = it[k].op.fill;
                 hseg[ns].status = dstat + it[k].idx;
                 hseg[ns].pad = 0;
-                nblocks += hseg[ns].nvec > 0 ? (hseg[ns].nvec + per_block - 1) / per_block : 1;
+                cls[nc].nblocks += hseg[ns].nvec > 0 ? hseg[ns].nvec : 1;
                 ns++;
             }
-        }
-        if (!err && ns > 0) {
-            pncxk_batch_args ba;
-            /* descriptors of one class live until its kernel ran: keep the
-             * copy and the launch on one stream, and sync before reuse */
-            err = pncxrt_memcpy_h2d(dseg, hseg, sizeof(pncxk_seg) * (size_t)ns, stream);
-            if (!err) {
-                ba.dsegs = dseg;
-                ba.nseg = ns;
-                ba.nblocks = nblocks;
-                ba.stream = stream;
-                err = pncxk_batch(op->kind, op->a, op->b, op->c, &ba);
-            }
-            if (!err) err = pncxrt_stream_sync(stream);
+            cls[nc].count = ns - cls[nc].first;
+            if (cls[nc].count > 0) nc++;
         }
         i = j;
     }
-    free(hseg);
+    /* pass 2: one descriptor upload, then the class launches */
+    if (!err && ns > 0) err = pncxrt_memcpy_h2d(dseg, hseg, sizeof(pncxk_seg) * (size_t)ns, stream);
+    for (k = 0; k < nc && !err; k++) {
+        pncxk_batch_args ba;
+        ba.dsegs = dseg + cls[k].first;
+        ba.nseg = cls[k].count;
+        ba.nblocks = cls[k].nblocks;
+        ba.stream = stream;
+        err = pncxk_batch(cls[k].op->kind, cls[k].op->a, cls[k].op->b, cls[k].op->c, &ba);
+    }
+    free(cls);
     return err;
 }
 
@@ -560,22 +555,21 @@ int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_
         nit++;
     }
     pthread_mutex_lock(&c->lock);
-    err = ensure_scratch(c, ALIGN16(sizeof(int) * (size_t)nseg) + sizeof(pncxk_seg) * (size_t)nseg + 16);
-    dstat = (int *)c->dscratch;
-    if (!err) err = pncxrt_memset(dstat, 0, sizeof(int) * (size_t)nseg, stream);
-    if (!err)
-        err = batch_launch(it, nit, dstat,
-                           (pncxk_seg *)((uint8_t *)c->dscratch + ALIGN16(sizeof(int) * (size_t)nseg)),
-                           stream);
-    if (!err) {
-        int *tmp = (int *)calloc((size_t)nseg, sizeof(int));
-        if (tmp == NULL) err = NC_ENOMEM;
-        if (!err) err = pncxrt_memcpy_d2h(tmp, dstat, sizeof(int) * (size_t)nseg, stream);
+    {
+        const size_t soff = ALIGN16(sizeof(int) * (size_t)nseg);
+        err = ensure_scratch(c, soff + sizeof(pncxk_seg) * (size_t)nseg + 16);
+        dstat = (int *)c->dscratch;
+        if (!err) err = pncxrt_memset(dstat, 0, sizeof(int) * (size_t)nseg, stream);
+        if (!err)
+            err = batch_launch(it, nit, dstat, (pncxk_seg *)((uint8_t *)c->dscratch + soff),
+                               (pncxk_seg *)((uint8_t *)c->hscratch + soff), stream);
+        /* statuses land in the pinned mirror (its descriptor part is no
+         * longer needed once the copy above has been ordered before) */
+        if (!err) err = pncxrt_memcpy_d2h(c->hscratch, dstat, sizeof(int) * (size_t)nseg, stream);
         if (!err) err = pncxrt_stream_sync(stream);
         if (!err)
             for (i = 0; i < nseg; i++)
-                if (hstat[i] == NC_NOERR) hstat[i] = tmp[i];
-        free(tmp);
+                if (hstat[i] == NC_NOERR) hstat[i] = ((int *)c->hscratch)[i];
     }
     pthread_mutex_unlock(&c->lock);
     if (!err)

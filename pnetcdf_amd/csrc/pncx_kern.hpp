@@ -147,8 +147,13 @@ __device__ __forceinline__ void vec_step(const uint8_t *src, uint8_t *dst,
 }
 
 __device__ __forceinline__ void publish_status(int *status, bool bad) {
+    if (status == nullptr) return;
     const unsigned long long m = __ballot(bad);
-    if (m != 0 && status != nullptr && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)m) - 1))
+    // Every out-of-range wave would otherwise store into the same word: with
+    // mostly-ERANGE data that serialises millions of atomics (measured 40 GB/s).
+    // Read first (relaxed, agent scope: L2) and store only if not yet set.
+    if (m != 0 && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)m) - 1) &&
+        __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != NC_ERANGE)
         __hip_atomic_store(status, NC_ERANGE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -188,6 +193,144 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t *src, uint8_t *dst
     publish_status(status, bad);
 }
 
+// ---------------------------------------------------------------------------
+// Tiled kernel (every op without the NULL-fill PRESERVE mode).  Measured on
+// MI355X: with nontemporal stores, a store instruction whose 64 lanes do not
+// cover one contiguous 1 KiB runs at half speed (int32->double 50% vs 83% of
+// HBM peak), so every global access below is contiguous per instruction:
+//   R = wide/narrow element size.
+//   R <= 2 (DIRECT): a lane converts E = 16/wide elements per tile: the wide
+//          side moves 16 B per lane, the narrow side 16/R B per lane.
+//   R >= 4 (LDS):    the narrow side moves 16 B per lane through a 4 KiB LDS
+//          tile; the wide side is R contiguous 1 KiB-per-wave instructions.
+// ---------------------------------------------------------------------------
+template <class Op>
+struct Shape {
+    static constexpr int SS = Op::SS, DS = Op::DS;
+    static constexpr int W = SS > DS ? SS : DS, N = SS < DS ? SS : DS, R = W / N;
+    static constexpr bool USE_LDS = R >= 4;
+    static constexpr int E = USE_LDS ? 16 / N : 16 / W;  // elements per lane per tile
+    static constexpr int TILE = 256 * E;                  // elements per block tile
+    static constexpr int E2 = 16 / W;                     // elements per wide 16 B chunk
+};
+
+template <int B> struct VecT;
+template <> struct VecT<16> { typedef uint32_t type __attribute__((ext_vector_type(4))); };
+template <> struct VecT<8> { typedef uint32_t type __attribute__((ext_vector_type(2))); };
+template <> struct VecT<4> { typedef uint32_t type; };
+template <> struct VecT<2> { typedef uint16_t type; };
+
+template <int B, bool NT>
+__device__ __forceinline__ typename VecT<B>::type ldv(const uint8_t *p) {
+    using V = typename VecT<B>::type;
+    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const V *>(p));
+    else return *reinterpret_cast<const V *>(p);
+}
+template <int B, bool NT>
+__device__ __forceinline__ void stv(uint8_t *p, typename VecT<B>::type v) {
+    using V = typename VecT<B>::type;
+    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<V *>(p));
+    else *reinterpret_cast<V *>(p) = v;
+}
+
+// convert K elements held as raw bytes (src layout) into raw bytes (dst layout)
+template <class Op, int K>
+__device__ __forceinline__ void conv_regs(const uint8_t *sb, uint8_t *db, typename Op::fill_t fill,
+                                          bool &bad) {
+    using SU = typename Op::SU;
+    using DU = typename Op::DU;
+    SU s[K];
+    DU d[K];
+    __builtin_memcpy(s, sb, sizeof s);
+#pragma unroll
+    for (int e = 0; e < K; e++) d[e] = Op::one(s[e], DU(0), fill, bad);
+    __builtin_memcpy(db, d, sizeof d);
+}
+
+// one full tile: src/dst point at the tile's first element
+template <class Op, bool NT>
+__device__ __forceinline__ void tile_body(const uint8_t *src, uint8_t *dst, typename Op::fill_t fill,
+                                          bool &bad, uint8_t *lds) {
+    using S = Shape<Op>;
+    constexpr int SS = S::SS, DS = S::DS;
+    const int lane = threadIdx.x;
+    if constexpr (!S::USE_LDS) {
+        constexpr int E = S::E, SB = E * SS, DB = E * DS;
+        alignas(16) uint8_t sb[SB];
+        alignas(16) uint8_t db[DB];
+        const auto v = ldv<SB, NT>(src + lane * SB);
+        __builtin_memcpy(sb, &v, SB);
+        conv_regs<Op, E>(sb, db, fill, bad);
+        typename VecT<DB>::type o;
+        __builtin_memcpy(&o, db, DB);
+        stv<DB, NT>(dst + lane * DB, o);
+    } else if constexpr (SS < DS) {
+        // widening: narrow src 16 B/lane -> LDS -> R wide 16 B chunks per lane
+        constexpr int R = S::R, E2 = S::E2;
+        const auto v = ldv<16, NT>(src + lane * 16);
+        *reinterpret_cast<typename VecT<16>::type *>(lds + lane * 16) = v;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const int c = k * 256 + lane;                      // wide chunk index
+            alignas(16) uint8_t sb[E2 * SS];
+            alignas(16) uint8_t db[16];
+            const auto w = *reinterpret_cast<const typename VecT<E2 * SS>::type *>(lds + c * E2 * SS);
+            __builtin_memcpy(sb, &w, E2 * SS);
+            conv_regs<Op, E2>(sb, db, fill, bad);
+            typename VecT<16>::type o;
+            __builtin_memcpy(&o, db, 16);
+            stv<16, NT>(dst + c * 16, o);
+        }
+    } else {
+        // narrowing: R wide 16 B chunks per lane -> LDS -> narrow 16 B/lane
+        constexpr int R = S::R, E2 = S::E2;
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const int c = k * 256 + lane;
+            alignas(16) uint8_t sb[16];
+            alignas(16) uint8_t db[E2 * DS];
+            const auto w = ldv<16, NT>(src + c * 16);
+            __builtin_memcpy(sb, &w, 16);
+            conv_regs<Op, E2>(sb, db, fill, bad);
+            typename VecT<E2 * DS>::type o;
+            __builtin_memcpy(&o, db, E2 * DS);
+            *reinterpret_cast<typename VecT<E2 * DS>::type *>(lds + c * E2 * DS) = o;
+        }
+        __syncthreads();
+        stv<16, NT>(dst + lane * 16, *reinterpret_cast<const typename VecT<16>::type *>(lds + lane * 16));
+    }
+}
+
+// scalar remainder [e0, n) by the 256 threads of one block
+template <class Op>
+__device__ __forceinline__ void scalar_range(const uint8_t *src, uint8_t *dst, int64_t e0, int64_t n,
+                                             typename Op::fill_t fill, bool &bad) {
+    for (int64_t e = e0 + threadIdx.x; e < n; e += 256) scalar_elem<Op>(src, dst, e, fill, bad);
+}
+
+template <class Op, bool NT>
+__global__ __launch_bounds__(256) void k_tile(const uint8_t *src, uint8_t *dst, int64_t head,
+                                              int64_t ntile, int64_t n, typename Op::fill_t fill,
+                                              int *status) {
+    using S = Shape<Op>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[S::USE_LDS ? 4096 : 16];
+    bool bad = false;
+    const int64_t nb = gridDim.x;
+    if (blockIdx.x == 0) {                               // scalar head and remainder
+        for (int64_t e = threadIdx.x; e < head; e += 256) scalar_elem<Op>(src, dst, e, fill, bad);
+        scalar_range<Op>(src, dst, head + ntile * S::TILE, n, fill, bad);
+    }
+    const uint8_t *ts = src + head * S::SS;
+    uint8_t *td = dst + head * S::DS;
+    for (int64_t t = xcd_remap(blockIdx.x, nb); t < ntile; t += nb) {
+        tile_body<Op, NT>(ts + t * (int64_t)S::TILE * S::SS, td + t * (int64_t)S::TILE * S::DS, fill, bad,
+                          lds);
+        if constexpr (S::USE_LDS) __syncthreads();       // LDS reuse in the next tile
+    }
+    publish_status(status, bad);
+}
+
 // fully scalar (misaligned buffers): one element per lane, byte-wise access
 template <class Op>
 __global__ __launch_bounds__(256) void k_scalar(const uint8_t *src, uint8_t *dst, int64_t n,
@@ -205,12 +348,15 @@ __global__ __launch_bounds__(256) void k_scalar(const uint8_t *src, uint8_t *dst
 // BATCH_STEPS vector steps of it (thread-strided inside the block, so each
 // wave-instruction still moves 1 KiB contiguously).
 // ---------------------------------------------------------------------------
-constexpr int BATCH_STEPS = 4;  // vector steps per lane per block
+// Block b serves tile (b - seg.block0) of the segment s with
+// seg[s].block0 <= b < seg[s+1].block0 (binary search over the sorted table);
+// the segment's first block also runs its scalar head and remainder.
+constexpr int BATCH_STEPS = 1;  // tiles per block
 
 template <class Op, bool NT>
 __global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg) {
-    constexpr int SB = Op::VEC * Op::SS, DB = Op::VEC * Op::DS;
-    // binary search for the segment of this block (segs sorted by block0)
+    using S = Shape<Op>;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[S::USE_LDS ? 4096 : 16];
     const long long b = blockIdx.x;
     int lo = 0, hi = nseg - 1;
     while (lo < hi) {
@@ -221,23 +367,16 @@ __global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg) 
     const uint8_t *src = (const uint8_t *)sg.src;
     uint8_t *dst = (uint8_t *)sg.dst;
     const typename Op::fill_t fill = sg.fill;
-    const int64_t nvec = sg.nvec;
+    const int64_t ntile = sg.nvec;     // full tiles
     bool bad = false;
-
     const int64_t rel = b - sg.block0;
-    if (rel == 0) {  // first block of the segment: scalar head and tail
-        const int64_t tail0 = sg.head + nvec * Op::VEC;
-        if (threadIdx.x < sg.head) scalar_elem<Op>(src, dst, threadIdx.x, fill, bad);
-        if (tail0 + threadIdx.x < sg.n) scalar_elem<Op>(src, dst, tail0 + threadIdx.x, fill, bad);
+    if (rel == 0) {
+        for (int64_t e = threadIdx.x; e < sg.head; e += 256) scalar_elem<Op>(src, dst, e, fill, bad);
+        scalar_range<Op>(src, dst, sg.head + ntile * S::TILE, sg.n, fill, bad);
     }
-    const uint8_t *vs = src + sg.head * Op::SS;
-    uint8_t *vd = dst + sg.head * Op::DS;
-    const int64_t v0 = rel * (int64_t)(BATCH_STEPS * 256);
-#pragma unroll
-    for (int u = 0; u < BATCH_STEPS; u++) {
-        const int64_t v = v0 + u * 256 + threadIdx.x;
-        if (v < nvec) vec_step<Op, NT>(vs + v * SB, vd + v * DB, fill, bad);
-    }
+    if (rel < ntile)
+        tile_body<Op, NT>(src + (sg.head + rel * (int64_t)S::TILE) * S::SS,
+                          dst + (sg.head + rel * (int64_t)S::TILE) * S::DS, fill, bad, lds);
     publish_status(sg.status, bad);
 }
 
@@ -263,21 +402,28 @@ int launch_stream(const pncxk_args *a) {
     const int64_t h = vec_head<Op>(a->src, a->dst, n);
     const uint8_t *src = (const uint8_t *)a->src;
     uint8_t *dst = (uint8_t *)a->dst;
+    const typename Op::fill_t fill = (typename Op::fill_t)a->fill;
     if (h < 0) {
         const int grid = launch_grid(n, 1);
-        hipLaunchKernelGGL((k_scalar<Op>), dim3(grid), dim3(256), 0, st, src, dst, n,
-                           (typename Op::fill_t)a->fill, a->status);
-    } else {
+        hipLaunchKernelGGL((k_scalar<Op>), dim3(grid), dim3(256), 0, st, src, dst, n, fill, a->status);
+    } else if constexpr (Op::PRESERVE) {
+        // NULL-fill codecs read xbuf: interleaved layout, plain stores
         const int64_t nvec = (n - h) / Op::VEC;
         int64_t grid = (nvec + 255) / 256;
         if (grid < 1) grid = 1;
         if (grid > MAX_BLOCKS) grid = MAX_BLOCKS;
+        hipLaunchKernelGGL((k_stream<Op, false>), dim3((unsigned)grid), dim3(256), 0, st, src, dst, h,
+                           nvec, n, fill, a->status);
+    } else {
+        const int64_t ntile = (n - h) / Shape<Op>::TILE;
+        int64_t grid = ntile < 1 ? 1 : ntile;
+        if (grid > MAX_BLOCKS) grid = MAX_BLOCKS;
         if (a->nontemporal >= 0)
-            hipLaunchKernelGGL((k_stream<Op, true>), dim3((unsigned)grid), dim3(256), 0, st, src, dst, h,
-                               nvec, n, (typename Op::fill_t)a->fill, a->status);
+            hipLaunchKernelGGL((k_tile<Op, true>), dim3((unsigned)grid), dim3(256), 0, st, src, dst, h,
+                               ntile, n, fill, a->status);
         else
-            hipLaunchKernelGGL((k_stream<Op, false>), dim3((unsigned)grid), dim3(256), 0, st, src, dst,
-                               h, nvec, n, (typename Op::fill_t)a->fill, a->status);
+            hipLaunchKernelGGL((k_tile<Op, false>), dim3((unsigned)grid), dim3(256), 0, st, src, dst, h,
+                               ntile, n, fill, a->status);
     }
     return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
 }
@@ -285,6 +431,7 @@ int launch_stream(const pncxk_args *a) {
 template <class Op>
 int launch_batch(const pncxk_batch_args *a) {
     if (a->nblocks <= 0) return 0;
+    if constexpr (Op::PRESERVE) return NC_EINVAL;   // host runs these one by one
     hipLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0,
                        (hipStream_t)a->stream, a->dsegs, a->nseg);
     return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
@@ -295,7 +442,7 @@ struct OpInfo {
     static void fill(pncxk_opinfo *o) {
         o->ss = Op::SS;
         o->ds = Op::DS;
-        o->vec = Op::VEC;
+        o->vec = Shape<Op>::TILE;     // elements per block tile
         o->batch_steps = BATCH_STEPS;
     }
 };
