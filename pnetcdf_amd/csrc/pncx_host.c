@@ -196,10 +196,7 @@ int pncx_dev_swapn(void *ddst, const void *dsrc, pncx_offset nelems, int esize,
     if (esize <= 0) return NC_EINVAL;
     if (nelems <= 0) return NC_NOERR;
     if (!have_device()) return PNCX_EDEVICE;
-    if (esize == 1) {
-        if (ddst == dsrc) return NC_NOERR;
-        return pncxrt_memcpy_d2d(ddst, dsrc, (size_t)nelems, stream);
-    }
+    if (esize == 1 && ddst == dsrc) return NC_NOERR;
     memset(&a, 0, sizeof a);
     a.src = dsrc;
     a.dst = ddst;
@@ -223,8 +220,7 @@ int pncx_dev_putn(int cdf_ver, int xtype, void *dxbuf, const void *dibuf, pncx_o
     if (err != NC_NOERR) return err;
     if (nelems <= 0) return NC_NOERR;
     if (!have_device()) return PNCX_EDEVICE;
-    if (op.kind == PNCXK_SWAP && op.a == 1)
-        return dxbuf == dibuf ? NC_NOERR : pncxrt_memcpy_d2d(dxbuf, dibuf, (size_t)nelems, stream);
+    if (op.kind == PNCXK_SWAP && op.a == 1 && dxbuf == dibuf) return NC_NOERR;
     return launch_op(&op, dibuf, dxbuf, nelems, dstatus, stream);
 }
 
@@ -236,8 +232,7 @@ int pncx_dev_getn(int cdf_ver, int xtype, const void *dxbuf, void *dibuf, pncx_o
     if (err != NC_NOERR) return err;
     if (nelems <= 0) return NC_NOERR;
     if (!have_device()) return PNCX_EDEVICE;
-    if (op.kind == PNCXK_SWAP && op.a == 1)
-        return dxbuf == dibuf ? NC_NOERR : pncxrt_memcpy_d2d(dibuf, dxbuf, (size_t)nelems, stream);
+    if (op.kind == PNCXK_SWAP && op.a == 1 && dxbuf == dibuf) return NC_NOERR;
     return launch_op(&op, dxbuf, dibuf, nelems, dstatus, stream);
 }
 
@@ -374,11 +369,8 @@ static int host_staged(const op_t *op, const void *src, void *dst, long long n, 
         err = pncxrt_memcpy_h2d(din, hs, (size_t)m * op->ss, s);
         if (!err && preserve && dout != din) err = pncxrt_memcpy_h2d(dout, hd, (size_t)m * op->ds, s);
         if (!err) {
-            if (op->kind == PNCXK_SWAP && op->a == 1) {
-                if (dout != din) err = pncxrt_memcpy_d2d(dout, din, (size_t)m, s);
-            } else {
+            if (!(op->kind == PNCXK_SWAP && op->a == 1 && dout == din))
                 err = launch_op(op, din, dout, m, c->dstatus + slot, s);
-            }
         }
         if (!err) err = pncxrt_memcpy_d2h(hd, dout, (size_t)m * op->ds, s);
     }
@@ -461,123 +453,192 @@ static long long seg_head(const void *src, const void *dst, int ss, int ds, long
     return -1;
 }
 
-/* Launch all items (device buffers) grouped by class; statuses go to
- * dstat[idx] (device ints, zeroed by the caller).  All tile descriptors are
- * planned first into the pinned mirror hseg, copied to the device in ONE
- * async copy, then every class is launched back to back on `stream`. */
-typedef struct cls_t { int first, count; long long nblocks; const op_t *op; } cls_t;
+/*
+ * Batched launch of device-buffer segments.
+ *   plan:  classify, group by conversion class (qsort), and for each class
+ *          lay out one tile descriptor per segment (16B-aligned body, scalar
+ *          head/remainder) with a running block offset;
+ *   run:   one async upload of all descriptors (pinned mirror), a block->
+ *          segment table built on the device for classes whose segments
+ *          differ in size (equal sizes need none), then the class kernels
+ *          back to back; statuses come back with one copy and one sync.
+ */
+typedef struct cls_t {
+    int first, count;       /* descriptor range                       */
+    long long nblocks;      /* grid of the class kernel               */
+    long long uniform;      /* blocks per segment when all are equal  */
+    long long map_off;      /* offset (ints) of its map in the map area, -1: none */
+    op_t op;
+} cls_t;
 
-static int batch_launch(bitem_t *it, int nit, int *dstat, pncxk_seg *dseg, pncxk_seg *hseg,
-                        void *stream)
+typedef struct plan_t {
+    bitem_t   *it;
+    int        nit;
+    pncxk_seg *seg;         /* host descriptors (later copied to the pinned mirror) */
+    int        nsegd;
+    cls_t     *cls;
+    int        ncls;
+    long long  map_ints;    /* total block-map ints */
+} plan_t;
+
+static void plan_free(plan_t *p)
 {
-    int i = 0, err = 0, ns = 0, nc = 0, k;
-    cls_t *cls = (cls_t *)malloc(sizeof(cls_t) * (size_t)(nit > 0 ? nit : 1));
-    if (cls == NULL) return NC_ENOMEM;
+    free(p->seg);
+    free(p->cls);
+    p->seg = NULL;
+    p->cls = NULL;
+}
+
+static int batch_plan(plan_t *p)
+{
+    int i = 0, err = 0, k;
+    bitem_t *it = p->it;
+    const int nit = p->nit;
+    p->seg = (pncxk_seg *)malloc(sizeof(pncxk_seg) * (size_t)(nit > 0 ? nit : 1));
+    p->cls = (cls_t *)malloc(sizeof(cls_t) * (size_t)(nit > 0 ? nit : 1));
+    p->nsegd = p->ncls = 0;
+    p->map_ints = 0;
+    if (p->seg == NULL || p->cls == NULL) return NC_ENOMEM;
     qsort(it, (size_t)nit, sizeof *it, cmp_item);
-    /* pass 1: launch what cannot be batched, plan the rest */
     while (!err && i < nit) {
         int j = i;
         pncxk_opinfo oi;
         const op_t *op = &it[i].op;
+        cls_t *c;
         while (j < nit && it[j].op.kind == op->kind && it[j].op.a == op->a &&
                it[j].op.b == op->b && it[j].op.c == op->c)
             j++;
-        if (op->kind == PNCXK_SWAP && op->a == 1) {            /* 1-byte copies */
-            for (k = i; k < j && !err; k++)
-                if (it[k].dst != it[k].src && it[k].n > 0)
-                    err = pncxrt_memcpy_d2d(it[k].dst, it[k].src, (size_t)it[k].n, stream);
-        } else if ((op->kind == PNCXK_SWAP && op->a != 2 && op->a != 4 && op->a != 8) || op->c) {
-            /* generic n-byte swaps and NULL-fill (PRESERVE) codecs: one launch each */
-            for (k = i; k < j && !err; k++)
-                err = launch_op(&it[k].op, it[k].src, it[k].dst, it[k].n, dstat + it[k].idx, stream);
-        } else if ((err = pncxk_opinfo_get(op->kind, op->a, op->b, op->c, &oi)) == 0) {
-            cls[nc].first = ns;
-            cls[nc].nblocks = 0;
-            cls[nc].op = op;
-            for (k = i; k < j && !err; k++) {
-                const long long h = seg_head(it[k].src, it[k].dst, oi.ss, oi.ds, it[k].n);
-                if (it[k].n <= 0) continue;
-                if (h < 0) {          /* cannot vectorise: own scalar launch */
-                    err = launch_op(&it[k].op, it[k].src, it[k].dst, it[k].n, dstat + it[k].idx, stream);
-                    continue;
-                }
-                hseg[ns].src = it[k].src;
-                hseg[ns].dst = it[k].dst;
-                hseg[ns].n = it[k].n;
-                hseg[ns].head = h;
-                hseg[ns].nvec = (it[k].n - h) / oi.vec;     /* full block tiles */
-                hseg[ns].block0 = cls[nc].nblocks;
-                hseg[ns].fill = it[k].op.fill;
-                hseg[ns].status = dstat + it[k].idx;
-                hseg[ns].pad = 0;
-                cls[nc].nblocks += hseg[ns].nvec > 0 ? hseg[ns].nvec : 1;
-                ns++;
+        if ((op->kind == PNCXK_SWAP && op->a != 1 && op->a != 2 && op->a != 4 && op->a != 8) ||
+            op->c || (err = pncxk_opinfo_get(op->kind, op->a, op->b, op->c, &oi)) != 0) {
+            i = j;          /* generic swaps / NULL-fill codecs: run one by one */
+            continue;
+        }
+        c = &p->cls[p->ncls];
+        c->first = p->nsegd;
+        c->nblocks = 0;
+        c->uniform = -1;
+        c->op = *op;
+        for (k = i; k < j; k++) {
+            pncxk_seg *sg;
+            long long nb;
+            const long long h = seg_head(it[k].src, it[k].dst, oi.ss, oi.ds, it[k].n);
+            if (it[k].n <= 0 || h < 0) continue;       /* empty / scalar-only: run alone */
+            sg = &p->seg[p->nsegd++];
+            sg->src = it[k].src;
+            sg->dst = it[k].dst;
+            sg->n = it[k].n;
+            sg->head = h;
+            sg->nvec = (it[k].n - h) / oi.vec;           /* full block tiles */
+            sg->block0 = c->nblocks;
+            sg->fill = it[k].op.fill;
+            sg->status = NULL;                           /* set at run time */
+            sg->pad = it[k].idx;                         /* caller's index  */
+            it[k].n = -it[k].n - 1;                      /* mark as batched */
+            nb = sg->nvec > 0 ? sg->nvec : 1;
+            if (c->uniform == -1) c->uniform = nb;
+            else if (c->uniform != nb) c->uniform = 0;
+            c->nblocks += nb;
+        }
+        c->count = p->nsegd - c->first;
+        if (c->count > 0) {
+            if (c->uniform <= 0) {
+                c->uniform = 0;
+                c->map_off = p->map_ints;
+                p->map_ints += c->nblocks;
+            } else {
+                c->map_off = -1;
             }
-            cls[nc].count = ns - cls[nc].first;
-            if (cls[nc].count > 0) nc++;
+            p->ncls++;
         }
         i = j;
     }
-    /* pass 2: one descriptor upload, then the class launches */
-    if (!err && ns > 0) err = pncxrt_memcpy_h2d(dseg, hseg, sizeof(pncxk_seg) * (size_t)ns, stream);
-    for (k = 0; k < nc && !err; k++) {
-        pncxk_batch_args ba;
-        ba.dsegs = dseg + cls[k].first;
-        ba.nseg = cls[k].count;
-        ba.nblocks = cls[k].nblocks;
-        ba.stream = stream;
-        err = pncxk_batch(cls[k].op->kind, cls[k].op->a, cls[k].op->b, cls[k].op->c, &ba);
+    return err;
+}
+
+static int batch_run(plan_t *p, int *dstat, pncxk_seg *dseg, pncxk_seg *hseg, int *dmap, void *stream)
+{
+    int k, err = 0;
+    /* items that are not in a class: one launch each */
+    for (k = 0; k < p->nit && !err; k++) {
+        bitem_t *b = &p->it[k];
+        if (b->n < 0) { b->n = -b->n - 1; continue; }        /* batched: restore */
+        if (b->n == 0) continue;
+        if (b->op.kind == PNCXK_SWAP && b->op.a == 1 && b->src == b->dst) continue;
+        err = launch_op(&b->op, b->src, b->dst, b->n, dstat + b->idx, stream);
     }
-    free(cls);
+    if (err || p->nsegd == 0) return err;
+    for (k = 0; k < p->nsegd; k++) {
+        p->seg[k].status = dstat + p->seg[k].pad;
+        p->seg[k].pad = 0;
+    }
+    memcpy(hseg, p->seg, sizeof(pncxk_seg) * (size_t)p->nsegd);
+    err = pncxrt_memcpy_h2d(dseg, hseg, sizeof(pncxk_seg) * (size_t)p->nsegd, stream);
+    for (k = 0; k < p->ncls && !err; k++) {
+        const cls_t *c = &p->cls[k];
+        pncxk_batch_args ba;
+        ba.dsegs = dseg + c->first;
+        ba.nseg = c->count;
+        ba.nblocks = c->nblocks;
+        ba.uniform = c->uniform;
+        ba.dmap = c->map_off >= 0 ? dmap + c->map_off : NULL;
+        ba.stream = stream;
+        if (ba.dmap != NULL) err = pncxk_batch_map(&ba);
+        if (!err) err = pncxk_batch(c->op.kind, c->op.a, c->op.b, c->op.c, &ba);
+    }
     return err;
 }
 
 int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_t stream)
 {
     ctx_t *c;
-    bitem_t *it;
-    int *dstat, *hstat, i, nit = 0, err = 0, first = NC_NOERR;
+    plan_t plan;
+    int *hstat, i, err = 0, first = NC_NOERR;
     if (nseg <= 0) return NC_NOERR;
     if (!have_device()) return PNCX_EDEVICE;
     c = get_ctx();
     if (c == NULL) return PNCX_EDEVICE;
-    it = (bitem_t *)calloc((size_t)nseg, sizeof *it);
+    memset(&plan, 0, sizeof plan);
+    plan.it = (bitem_t *)calloc((size_t)nseg, sizeof *plan.it);
     hstat = (int *)calloc((size_t)nseg, sizeof(int));
-    if (it == NULL || hstat == NULL) { free(it); free(hstat); return NC_ENOMEM; }
+    if (plan.it == NULL || hstat == NULL) { free(plan.it); free(hstat); return NC_ENOMEM; }
     for (i = 0; i < nseg; i++) {
         const pncx_seg *s = &segs[i];
-        int e = classify(s->dir, s->cdf_ver, s->xtype, s->itype, s->fillp, &it[nit].op);
+        bitem_t *b = &plan.it[plan.nit];
+        int e = classify(s->dir, s->cdf_ver, s->xtype, s->itype, s->fillp, &b->op);
         if (e != NC_NOERR) { hstat[i] = e; continue; }
-        it[nit].idx = i;
-        it[nit].n = s->nelems;
-        it[nit].src = s->dir == PNCX_PUT ? s->ibuf : s->xbuf;
-        it[nit].dst = s->dir == PNCX_PUT ? s->xbuf : s->ibuf;
-        nit++;
+        b->idx = i;
+        b->n = s->nelems > 0 ? s->nelems : 0;
+        b->src = s->dir == PNCX_PUT ? s->ibuf : s->xbuf;
+        b->dst = s->dir == PNCX_PUT ? s->xbuf : s->ibuf;
+        plan.nit++;
     }
+    err = batch_plan(&plan);
     pthread_mutex_lock(&c->lock);
-    {
+    if (!err) {
+        /* scratch layout: [statuses | descriptors | block maps] */
         const size_t soff = ALIGN16(sizeof(int) * (size_t)nseg);
-        err = ensure_scratch(c, soff + sizeof(pncxk_seg) * (size_t)nseg + 16);
-        dstat = (int *)c->dscratch;
-        if (!err) err = pncxrt_memset(dstat, 0, sizeof(int) * (size_t)nseg, stream);
+        const size_t moff = soff + ALIGN16(sizeof(pncxk_seg) * (size_t)(plan.nsegd + 1));
+        err = ensure_scratch(c, moff + sizeof(int) * (size_t)plan.map_ints + 16);
+        if (!err) err = pncxrt_memset(c->dscratch, 0, sizeof(int) * (size_t)nseg, stream);
         if (!err)
-            err = batch_launch(it, nit, dstat, (pncxk_seg *)((uint8_t *)c->dscratch + soff),
-                               (pncxk_seg *)((uint8_t *)c->hscratch + soff), stream);
-        /* statuses land in the pinned mirror (its descriptor part is no
-         * longer needed once the copy above has been ordered before) */
-        if (!err) err = pncxrt_memcpy_d2h(c->hscratch, dstat, sizeof(int) * (size_t)nseg, stream);
+            err = batch_run(&plan, (int *)c->dscratch, (pncxk_seg *)((uint8_t *)c->dscratch + soff),
+                            (pncxk_seg *)((uint8_t *)c->hscratch + soff),
+                            (int *)((uint8_t *)c->dscratch + moff), stream);
+        /* statuses land in the pinned mirror's status area */
+        if (!err) err = pncxrt_memcpy_d2h(c->hscratch, c->dscratch, sizeof(int) * (size_t)nseg, stream);
         if (!err) err = pncxrt_stream_sync(stream);
         if (!err)
             for (i = 0; i < nseg; i++)
                 if (hstat[i] == NC_NOERR) hstat[i] = ((int *)c->hscratch)[i];
     }
     pthread_mutex_unlock(&c->lock);
+    plan_free(&plan);
     if (!err)
         for (i = 0; i < nseg; i++) {
             if (status_out) status_out[i] = hstat[i];
             if (first == NC_NOERR) first = hstat[i];
         }
-    free(it);
+    free(plan.it);
     free(hstat);
     return err ? (err < 0 ? err : PNCX_EDEVICE) : first;
 }

@@ -208,7 +208,8 @@ template <class Op>
 struct Shape {
     static constexpr int SS = Op::SS, DS = Op::DS;
     static constexpr int W = SS > DS ? SS : DS, N = SS < DS ? SS : DS, R = W / N;
-    static constexpr bool USE_LDS = R >= 4;
+    // narrowing 2:1 also stages (16 B stores per lane instead of 8 B)
+    static constexpr bool USE_LDS = R >= 4 || (R == 2 && SS > DS);
     static constexpr int E = USE_LDS ? 16 / N : 16 / W;  // elements per lane per tile
     static constexpr int TILE = 256 * E;                  // elements per block tile
     static constexpr int E2 = 16 / W;                     // elements per wide 16 B chunk
@@ -354,14 +355,23 @@ __global__ __launch_bounds__(256) void k_scalar(const uint8_t *src, uint8_t *dst
 constexpr int BATCH_STEPS = 1;  // tiles per block
 
 template <class Op, bool NT>
-__global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg) {
+__global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg, long long uniform,
+                                               const int *map) {
     using S = Shape<Op>;
     __shared__ __attribute__((aligned(16))) uint8_t lds[S::USE_LDS ? 4096 : 16];
     const long long b = blockIdx.x;
-    int lo = 0, hi = nseg - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (segs[mid].block0 <= b) lo = mid; else hi = mid - 1;
+    int lo;
+    if (uniform > 0) {                     // equal-size segments: direct
+        lo = (int)(b / uniform);
+    } else if (map != nullptr) {           // block -> segment table
+        lo = map[b];
+    } else {                               // binary search (sorted by block0)
+        int hi = nseg - 1;
+        lo = 0;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (segs[mid].block0 <= b) lo = mid; else hi = mid - 1;
+        }
     }
     const pncxk_seg sg = segs[lo];
     const uint8_t *src = (const uint8_t *)sg.src;
@@ -433,7 +443,7 @@ int launch_batch(const pncxk_batch_args *a) {
     if (a->nblocks <= 0) return 0;
     if constexpr (Op::PRESERVE) return NC_EINVAL;   // host runs these one by one
     hipLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0,
-                       (hipStream_t)a->stream, a->dsegs, a->nseg);
+                       (hipStream_t)a->stream, a->dsegs, a->nseg, a->uniform, a->dmap);
     return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
 }
 

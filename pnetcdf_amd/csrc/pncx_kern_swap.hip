@@ -104,6 +104,24 @@ extern "C" int pncxk_batch(int kind, int a, int b, int c, const pncxk_batch_args
     return NC_EINVAL;
 }
 
+// block -> segment table for non-uniform batches: block s of this grid
+// writes s into [seg[s].block0, seg[s].block0 + nblocks(s))
+static __global__ __launch_bounds__(256) void k_batch_map(const pncxk_seg *segs, int nseg, long long nblocks,
+                                                   int *map) {
+    const int s = blockIdx.x;
+    if (s >= nseg) return;
+    const long long b0 = segs[s].block0;
+    const long long b1 = s + 1 < nseg ? segs[s + 1].block0 : nblocks;
+    for (long long b = b0 + threadIdx.x; b < b1; b += 256) map[b] = s;
+}
+
+extern "C" int pncxk_batch_map(const pncxk_batch_args *a) {
+    if (a->nseg <= 0 || a->dmap == nullptr) return 0;
+    hipLaunchKernelGGL(k_batch_map, dim3((unsigned)a->nseg), dim3(256), 0, (hipStream_t)a->stream,
+                       a->dsegs, a->nseg, a->nblocks, a->dmap);
+    return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
+}
+
 extern "C" int pncxk_opinfo_get(int kind, int a, int b, int c, pncxk_opinfo *o) {
     if (kind == PNCXK_SWAP) {
         switch (a) {

@@ -37,9 +37,11 @@ typedef struct pncxk_seg {
 } pncxk_seg;
 
 typedef struct pncxk_batch_args {
-    const pncxk_seg *dsegs;    /* device array, sorted by block0 */
+    const pncxk_seg *dsegs;    /* device array, sorted by block0           */
     int              nseg;
     long long        nblocks;
+    long long        uniform;  /* blocks per segment if all equal, else 0  */
+    int             *dmap;     /* device block->segment table or NULL      */
     void            *stream;
 } pncxk_batch_args;
 
@@ -62,6 +64,8 @@ int pncxk_get(int xtype, int itype, const pncxk_args *a);
 int pncxk_put(int xtype, int itype, int preserve, const pncxk_args *a);
 int pncxk_batch(int kind, int a, int b, int c, const pncxk_batch_args *args);
 int pncxk_opinfo_get(int kind, int a, int b, int c, pncxk_opinfo *o);
+/* fill args->dmap (nblocks ints) from the device descriptors */
+int pncxk_batch_map(const pncxk_batch_args *args);
 
 /* ---- HIP runtime wrappers (return 0 on success, PNCX_EDEVICE on error) ---- */
 int  pncxrt_device_count(void);
