@@ -104,15 +104,20 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from pnetcdf_amd import nctypes as T
     from pnetcdf_amd import pncx
+    from pnetcdf_amd.shard import Group, record_slab
     lib = pncx.lib()
+    group = Group(dist, torch.device("cuda", local))
     stream = torch.cuda.current_stream()
     sptr = ctypes.c_void_p(stream.cuda_stream)
 
     # ---------------------------------------------------------- workload
     if args.workload == "c2":
         n = int(args.slab_gib * GIB) // 8                      # NC_DOUBLE elements per rank
+        rec_elems = 8192 * 16384                               # one 1 GiB record of v(time, 8192, 16384)
+        nrec_total = (n // rec_elems) * world
+        first_rec, my_recs = record_slab(nrec_total, world, rank)
         buf = torch.empty(n, dtype=torch.int64, device="cuda")
-        splitmix64_fill(torch, buf, SEEDS["c5" if world > 1 else "c2"] + rank)
+        splitmix64_fill(torch, buf, SEEDS["c5" if world > 1 else "c2"] + first_rec)
         ptr = ctypes.c_void_p(buf.data_ptr())
         bytes_per_elem = 16                                    # 8 R + 8 W
 
@@ -122,9 +127,9 @@ def main():
         elems = n
         metric_key = "swap8"
         dtype = "u64"
-        recs = n * 8 // (1 << 30)
+        recs = my_recs
         cfg = {"workload": ("C2: 32 GiB contiguous NC_DOUBLE get_vara, in-place 8-byte swap" if world == 1 else
-                            f"C5: NC_DOUBLE record variable v(time={recs * world}, 8192, 16384), "
+                            f"C5: NC_DOUBLE record variable v(time={nrec_total}, 8192, 16384), "
                             f"{recs} x 1 GiB records per GPU, in-place 8-byte swap"),
                "slab_gib_per_gpu": args.slab_gib, "elements_per_gpu": n, "xtype": "NC_DOUBLE",
                "itype": "double", "records_per_gpu": recs,
@@ -180,8 +185,7 @@ def main():
     # ---------------------------------------------------------- timed region
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
-    if dist is not None:
-        dist.barrier()
+    group.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -189,14 +193,10 @@ def main():
         launch()
         evs[k][1].record(stream)
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
+    group.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-    if dist is not None:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+    elapsed, kern_ms = group.max([elapsed, kern_ms])         # max over ranks
 
     moved = float(bytes_per_elem) * elems * world * args.steps
     value = moved / elapsed / GIB

@@ -1,0 +1,77 @@
+"""Record-slab sharding of a request across the GPUs of one node (config 5).
+
+A record variable's records are independent and, for a single record
+variable, contiguous in the file (record r starts at begin + r*recsize with
+recsize = the record's own size, ncmpio_enddef.c:586-607).  The reference
+splits a record request into per-record sub-requests
+(ncmpio_i_getput.m4:332,416); here each rank (one GPU) takes one contiguous
+slab of records and converts it with no data-path communication.  The only
+exchanges are control: a barrier around the timed region, the max of the
+per-rank times, and the "first error" of the conversions (NC_ERANGE is the
+only error a conversion produces, so the minimum status over ranks is the
+reference's first-error semantics, ncx.m4:2487-2488).
+
+The same helpers run over RCCL (backend "nccl", device tensors) in bench.py
+and over gloo (CPU tensors) in tests/test_shard_gloo.py.
+"""
+
+
+def record_slab(nrecs, world, rank):
+    """Balanced contiguous partition of nrecs records: (first, count)."""
+    if world <= 0 or not (0 <= rank < world):
+        raise ValueError("bad rank/world")
+    base, rem = divmod(nrecs, world)
+    first = rank * base + min(rank, rem)
+    return first, base + (1 if rank < rem else 0)
+
+
+def record_extent(begin, recsize, first, count):
+    """Byte range [start, end) of records first..first+count-1 of a single
+    record variable in the file."""
+    return begin + first * recsize, begin + (first + count) * recsize
+
+
+class Group:
+    """Control-plane collectives for the sharded run (no data movement)."""
+
+    def __init__(self, dist=None, device="cpu"):
+        self.dist = dist
+        self.device = device
+
+    @property
+    def world(self):
+        return self.dist.get_world_size() if self.dist is not None else 1
+
+    @property
+    def rank(self):
+        return self.dist.get_rank() if self.dist is not None else 0
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max(self, values):
+        """Element-wise max over ranks of a list of floats."""
+        if self.dist is None:
+            return list(values)
+        import torch
+        t = torch.tensor(list(values), dtype=torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return [float(v) for v in t.cpu()]
+
+    def sum(self, values):
+        if self.dist is None:
+            return list(values)
+        import torch
+        t = torch.tensor(list(values), dtype=torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return [float(v) for v in t.cpu()]
+
+    def first_error(self, status):
+        """min over ranks of an NC status (0 = NC_NOERR, negatives = errors)."""
+        if self.dist is None:
+            return int(status)
+        import torch
+        t = torch.tensor([int(status)], dtype=torch.int64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        return int(t.item())
