@@ -96,17 +96,24 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("PNCX_DIST_BACKEND", "nccl") != "nccl":
+        local = 0          # rehearsal: every rank on GPU 0
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("PNCX_DIST_BACKEND", "nccl")   # nccl == RCCL on ROCm
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:   # rehearsal of the N>1 path with several ranks on one GPU
+            dist.init_process_group(backend)
     from pnetcdf_amd import nctypes as T
     from pnetcdf_amd import pncx
     from pnetcdf_amd.shard import Group, record_slab
     lib = pncx.lib()
-    group = Group(dist, torch.device("cuda", local))
+    group = Group(dist, torch.device("cuda", local) if os.environ.get("PNCX_DIST_BACKEND", "nccl") == "nccl"
+                  else "cpu")
     stream = torch.cuda.current_stream()
     sptr = ctypes.c_void_p(stream.cuda_stream)
 

@@ -434,13 +434,23 @@ typedef struct bitem_t {
     long long   n;
 } bitem_t;
 
+static int mixable(const op_t *o)
+{
+    return o->kind == PNCXK_SWAP && (o->a == 1 || o->a == 2 || o->a == 4 || o->a == 8);
+}
+
+/* order: mixable same-type swaps first (one class), then by conversion class */
 static int cmp_item(const void *pa, const void *pb)
 {
     const bitem_t *a = (const bitem_t *)pa, *b = (const bitem_t *)pb;
-    if (a->op.kind != b->op.kind) return a->op.kind - b->op.kind;
-    if (a->op.a != b->op.a) return a->op.a - b->op.a;
-    if (a->op.b != b->op.b) return a->op.b - b->op.b;
-    if (a->op.c != b->op.c) return a->op.c - b->op.c;
+    const int ma = mixable(&a->op), mb = mixable(&b->op);
+    if (ma != mb) return mb - ma;
+    if (!ma) {
+        if (a->op.kind != b->op.kind) return a->op.kind - b->op.kind;
+        if (a->op.a != b->op.a) return a->op.a - b->op.a;
+        if (a->op.b != b->op.b) return a->op.b - b->op.b;
+        if (a->op.c != b->op.c) return a->op.c - b->op.c;
+    }
     return a->idx - b->idx;
 }
 
@@ -501,16 +511,19 @@ static int batch_plan(plan_t *p)
     if (p->seg == NULL || p->cls == NULL) return NC_ENOMEM;
     qsort(it, (size_t)nit, sizeof *it, cmp_item);
     while (!err && i < nit) {
-        int j = i;
+        int j = i, mix;
         pncxk_opinfo oi;
         const op_t *op = &it[i].op;
         cls_t *c;
-        while (j < nit && it[j].op.kind == op->kind && it[j].op.a == op->a &&
-               it[j].op.b == op->b && it[j].op.c == op->c)
+        /* all same-type swaps/copies of 1/2/4/8 bytes form ONE class (one
+         * launch); other classes are one (kind, xtype, itype) each */
+        mix = mixable(op);
+        while (j < nit && (mix ? mixable(&it[j].op)
+                               : (it[j].op.kind == op->kind && it[j].op.a == op->a &&
+                                  it[j].op.b == op->b && it[j].op.c == op->c)))
             j++;
-        if ((op->kind == PNCXK_SWAP && op->a != 1 && op->a != 2 && op->a != 4 && op->a != 8) ||
-            op->c || (err = pncxk_opinfo_get(op->kind, op->a, op->b, op->c, &oi)) != 0) {
-            i = j;          /* generic swaps / NULL-fill codecs: run one by one */
+        if ((op->kind == PNCXK_SWAP && !mix) || op->c) {
+            i = j;          /* generic n-byte swaps / NULL-fill codecs: run one by one */
             continue;
         }
         c = &p->cls[p->ncls];
@@ -518,11 +531,14 @@ static int batch_plan(plan_t *p)
         c->nblocks = 0;
         c->uniform = -1;
         c->op = *op;
-        for (k = i; k < j; k++) {
+        if (mix) c->op.kind = PNCXK_SWAPMIX;
+        for (k = i; k < j && !err; k++) {
             pncxk_seg *sg;
-            long long nb;
-            const long long h = seg_head(it[k].src, it[k].dst, oi.ss, oi.ds, it[k].n);
+            long long nb, h;
+            if ((err = pncxk_opinfo_get(it[k].op.kind, it[k].op.a, it[k].op.b, it[k].op.c, &oi)) != 0) break;
+            h = seg_head(it[k].src, it[k].dst, oi.ss, oi.ds, it[k].n);
             if (it[k].n <= 0 || h < 0) continue;       /* empty / scalar-only: run alone */
+            if (mix && it[k].src == it[k].dst && it[k].op.a == 1) { it[k].n = -it[k].n - 1; continue; }
             sg = &p->seg[p->nsegd++];
             sg->src = it[k].src;
             sg->dst = it[k].dst;
@@ -531,8 +547,8 @@ static int batch_plan(plan_t *p)
             sg->nvec = (it[k].n - h) / oi.vec;           /* full block tiles */
             sg->block0 = c->nblocks;
             sg->fill = it[k].op.fill;
-            sg->status = NULL;                           /* set at run time */
-            sg->pad = it[k].idx;                         /* caller's index  */
+            sg->status = (int *)(intptr_t)it[k].idx;     /* caller's index; pointer set at run time */
+            sg->aux = it[k].op.a;
             it[k].n = -it[k].n - 1;                      /* mark as batched */
             nb = sg->nvec > 0 ? sg->nvec : 1;
             if (c->uniform == -1) c->uniform = nb;
@@ -555,9 +571,23 @@ static int batch_plan(plan_t *p)
     return err;
 }
 
-static int batch_run(plan_t *p, int *dstat, pncxk_seg *dseg, pncxk_seg *hseg, int *dmap, void *stream)
+/* scratch layout (device and pinned mirror): [statuses | descriptors | maps].
+ * ONE upload zeroes the statuses and installs the descriptors; then the
+ * unbatched items and the class kernels run; one copy brings the statuses back. */
+static int batch_run(plan_t *p, int nseg, uint8_t *dbase, uint8_t *hbase, size_t soff, size_t moff,
+                     void *stream)
 {
     int k, err = 0;
+    int *dstat = (int *)dbase;
+    pncxk_seg *dseg = (pncxk_seg *)(dbase + soff), *hseg = (pncxk_seg *)(hbase + soff);
+    int *dmap = (int *)(dbase + moff);
+    memset(hbase, 0, soff);
+    for (k = 0; k < p->nsegd; k++) {
+        hseg[k] = p->seg[k];
+        hseg[k].status = dstat + (intptr_t)p->seg[k].status;
+    }
+    err = pncxrt_memcpy_h2d(dbase, hbase, soff + sizeof(pncxk_seg) * (size_t)p->nsegd, stream);
+    (void)nseg;
     /* items that are not in a class: one launch each */
     for (k = 0; k < p->nit && !err; k++) {
         bitem_t *b = &p->it[k];
@@ -566,13 +596,6 @@ static int batch_run(plan_t *p, int *dstat, pncxk_seg *dseg, pncxk_seg *hseg, in
         if (b->op.kind == PNCXK_SWAP && b->op.a == 1 && b->src == b->dst) continue;
         err = launch_op(&b->op, b->src, b->dst, b->n, dstat + b->idx, stream);
     }
-    if (err || p->nsegd == 0) return err;
-    for (k = 0; k < p->nsegd; k++) {
-        p->seg[k].status = dstat + p->seg[k].pad;
-        p->seg[k].pad = 0;
-    }
-    memcpy(hseg, p->seg, sizeof(pncxk_seg) * (size_t)p->nsegd);
-    err = pncxrt_memcpy_h2d(dseg, hseg, sizeof(pncxk_seg) * (size_t)p->nsegd, stream);
     for (k = 0; k < p->ncls && !err; k++) {
         const cls_t *c = &p->cls[k];
         pncxk_batch_args ba;
@@ -619,11 +642,8 @@ int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_
         const size_t soff = ALIGN16(sizeof(int) * (size_t)nseg);
         const size_t moff = soff + ALIGN16(sizeof(pncxk_seg) * (size_t)(plan.nsegd + 1));
         err = ensure_scratch(c, moff + sizeof(int) * (size_t)plan.map_ints + 16);
-        if (!err) err = pncxrt_memset(c->dscratch, 0, sizeof(int) * (size_t)nseg, stream);
         if (!err)
-            err = batch_run(&plan, (int *)c->dscratch, (pncxk_seg *)((uint8_t *)c->dscratch + soff),
-                            (pncxk_seg *)((uint8_t *)c->hscratch + soff),
-                            (int *)((uint8_t *)c->dscratch + moff), stream);
+            err = batch_run(&plan, nseg, (uint8_t *)c->dscratch, (uint8_t *)c->hscratch, soff, moff, stream);
         /* statuses land in the pinned mirror's status area */
         if (!err) err = pncxrt_memcpy_d2h(c->hscratch, c->dscratch, sizeof(int) * (size_t)nseg, stream);
         if (!err) err = pncxrt_stream_sync(stream);

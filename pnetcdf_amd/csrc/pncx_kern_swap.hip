@@ -89,7 +89,48 @@ extern "C" int pncxk_batch_get(int xtype, int itype, const pncxk_batch_args *a);
 extern "C" int pncxk_batch_put(int xtype, int itype, int preserve, const pncxk_batch_args *a);
 extern "C" int pncxk_opinfo_getput(int kind, int xtype, int itype, int preserve, pncxk_opinfo *o);
 
+// One launch for all same-type segments of a batch (C4: NC_SHORT and
+// NC_FLOAT iputs): the block's segment says its element size; the tile body
+// is the same as for the single-size classes.
+template <bool NT>
+__global__ __launch_bounds__(256) void k_batch_swapmix(const pncxk_seg *segs, int nseg, long long uniform,
+                                                       const int *map) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[16];
+    const long long b = blockIdx.x;
+    const int s = uniform > 0 ? (int)(b / uniform) : map[b];
+    const pncxk_seg sg = segs[s];
+    const uint8_t *src = (const uint8_t *)sg.src;
+    uint8_t *dst = (uint8_t *)sg.dst;
+    const int64_t rel = b - sg.block0;
+    bool bad = false;
+    switch (sg.aux) {
+#define PNCX_MIX(ES)                                                                               \
+        case ES: {                                                                                 \
+            using Op = SwapOp<ES>;                                                                 \
+            using S = Shape<Op>;                                                                   \
+            if (rel == 0) {                                                                        \
+                for (int64_t e = threadIdx.x; e < sg.head; e += 256) scalar_elem<Op>(src, dst, e, 0, bad); \
+                scalar_range<Op>(src, dst, sg.head + sg.nvec * S::TILE, sg.n, 0, bad);            \
+            }                                                                                      \
+            if (rel < sg.nvec)                                                                     \
+                tile_body<Op, NT>(src + (sg.head + rel * (int64_t)S::TILE) * ES,                   \
+                                  dst + (sg.head + rel * (int64_t)S::TILE) * ES, 0, bad, lds);     \
+            break;                                                                                 \
+        }
+        PNCX_MIX(1) PNCX_MIX(2) PNCX_MIX(4) PNCX_MIX(8)
+#undef PNCX_MIX
+        default: break;
+    }
+    (void)nseg;
+}
+
 extern "C" int pncxk_batch(int kind, int a, int b, int c, const pncxk_batch_args *args) {
+    if (kind == PNCXK_SWAPMIX) {
+        if (args->nblocks <= 0) return 0;
+        hipLaunchKernelGGL((k_batch_swapmix<true>), dim3((unsigned)args->nblocks), dim3(256), 0,
+                           (hipStream_t)args->stream, args->dsegs, args->nseg, args->uniform, args->dmap);
+        return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
+    }
     if (kind == PNCXK_SWAP) {
         switch (a) {
             case 1: return launch_batch<SwapOp<1>>(args);

@@ -33,7 +33,7 @@ typedef struct pncxk_seg {
     long long          block0; /* first block of this segment                 */
     unsigned long long fill;
     int               *status; /* device int of this segment, or NULL         */
-    int                pad;
+    int                aux;    /* SWAPMIX: element size of this segment       */
 } pncxk_seg;
 
 typedef struct pncxk_batch_args {
@@ -56,6 +56,7 @@ typedef struct pncxk_opinfo {
 #define PNCXK_SWAP 0  /* a = esize (1 = copy)  */
 #define PNCXK_GET  1  /* a = xtype, b = itype  */
 #define PNCXK_PUT  2  /* a = xtype, b = itype, c = preserve */
+#define PNCXK_SWAPMIX 3  /* batch only: same-type swaps/copies of any of 1/2/4/8 bytes */
 
 /* ---- kernel launchers (HIP TUs) ---- */
 int pncxk_swap(int esize, const pncxk_args *a);          /* esize 1,2,4,8 */

@@ -153,15 +153,9 @@ int main(int argc, char **argv) {
 
 #define ONE2(U, NT, BS, XM) { const int64_t g = (nvec + (int64_t)BS * U - 1) / ((int64_t)BS * U); \
       add(std::string("one2 U") + #U + " nt" + #NT + " bs" + #BS + " xcd" + #XM, 2, [=] { hipLaunchKernelGGL((k_one2<U, NT, BS, XM>), dim3(g), dim3(BS), 0, 0, p, nvec); }); }
-    ONE2(1, false, 256, false) ONE2(1, true, 256, false) ONE2(1, false, 256, true)
-    ONE2(1, false, 512, false) ONE2(1, false, 1024, false) ONE2(1, false, 128, false) ONE2(1, false, 64, false)
-    ONE2(2, false, 256, false) ONE2(2, true, 256, false) ONE2(2, false, 512, false)
-    ONE2(1, true, 512, false) ONE2(1, true, 1024, false) ONE2(1, true, 256, true)
-    { const int64_t g = (nvec + 511) / 512; add("consec U2 nt0", 2, [=] { hipLaunchKernelGGL((k_one_consec<2, false>), dim3(g), dim3(256), 0, 0, p, nvec); }); }
-    { const int64_t g = (nvec + 1023) / 1024; add("consec U4 nt0", 2, [=] { hipLaunchKernelGGL((k_one_consec<4, false>), dim3(g), dim3(256), 0, 0, p, nvec); }); }
-    { const int64_t g = (nvec + 511) / 512; add("consec U2 nt1", 2, [=] { hipLaunchKernelGGL((k_one_consec<2, true>), dim3(g), dim3(256), 0, 0, p, nvec); }); }
-    { const int g = cus; add("gs U4 nt1 bpc1", 2, [=] { hipLaunchKernelGGL((k_gs<4, true>), dim3(g), dim3(256), 0, 0, p, nvec); }); }
-    { const int g8 = cus * 8; add("copy (out-of-place) bpc8", 2, [=] { hipLaunchKernelGGL(k_copy, dim3(g8), dim3(256), 0, 0, p, q, nvec); }); }
+    ONE2(1, true, 256, true) ONE2(1, true, 128, true) ONE2(1, true, 64, true) ONE2(1, true, 512, true)
+    ONE2(1, true, 1024, true) ONE2(2, true, 256, true) ONE2(2, true, 128, true) ONE2(2, true, 64, true)
+    ONE2(4, true, 64, true) ONE2(1, false, 64, true) ONE2(1, false, 128, true)
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
