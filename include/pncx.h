@@ -185,6 +185,28 @@ int pncx_dev_getn(int cdf_ver, int xtype, const void *dxbuf, void *dibuf,
                   pncx_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
+/* varm: internal buffer laid out by imap[] (element strides per dimension,  */
+/* ncmpii_create_imaptype, src/drivers/common/create_imaptype.c:25-139),     */
+/* external buffer contiguous row-major over count[].  Replaces the MPI_Pack */
+/* / MPI_Unpack by the imap type followed by the conversion                 */
+/* (ncmpio_util.c:654-689 + 716-765, unpack :842-966) with ONE fused gather  */
+/* (put) or scatter (get) kernel.  ndims <= 16; imap[d] >= 0.  For get, the  */
+/* imap must not map two packed elements to one user element (the scatter    */
+/* order is unspecified, where MPI_Unpack's last-write-wins is not).         */
+/* ------------------------------------------------------------------------ */
+int pncx_dev_putn_imap(int cdf_ver, int xtype, void *dxbuf, const void *dibuf, int ndims,
+                       const pncx_offset *count, const pncx_offset *imap, int itype,
+                       const void *fillp, int *dstatus, pncx_stream_t stream);
+int pncx_dev_getn_imap(int cdf_ver, int xtype, const void *dxbuf, void *dibuf, int ndims,
+                       const pncx_offset *count, const pncx_offset *imap, int itype,
+                       int *dstatus, pncx_stream_t stream);
+/* host buffers: the user-buffer span sum((count-1)*imap)+1 elements is staged */
+int pncx_putn_imap(int cdf_ver, int xtype, void *xbuf, const void *ibuf, int ndims,
+                   const pncx_offset *count, const pncx_offset *imap, int itype, const void *fillp);
+int pncx_getn_imap(int cdf_ver, int xtype, const void *xbuf, void *ibuf, int ndims,
+                   const pncx_offset *count, const pncx_offset *imap, int itype);
+
+/* ------------------------------------------------------------------------ */
 /* Batched conversion: many independent requests in one launch per         */
 /* conversion class (replaces the per-request loop of                       */
 /* ncmpio_igetput_varm, ncmpio_i_getput.m4:300-303, and the per-request      */

@@ -424,6 +424,151 @@ int pncx_getn(int cdf_ver, int xtype, const void *xbuf, void *ibuf, pncx_offset 
 }
 
 /* ------------------------------------------------------------------------ */
+/* varm (imap) fused gather/scatter + conversion                             */
+/* ------------------------------------------------------------------------ */
+/* Mirrors ncmpii_create_imaptype (create_imaptype.c:25-139): returns 1 with
+ * *n = number of elements when imap[] is a true (non-contiguous) varm layout,
+ * 0 when it is plain C order (then the contiguous kernels apply). */
+static int imap_layout(int ndims, const pncx_offset *count, const pncx_offset *imap, pncxk_imap *m,
+                       long long *n, long long *span, int *err)
+{
+    int d;
+    long long blk = 1, total = 1, sp = 0;
+    *err = NC_NOERR;
+    if (ndims < 0 || ndims > PNCX_MAX_DIMS) { *err = NC_EINVAL; return 0; }
+    memset(m, 0, sizeof *m);
+    for (d = 0; d < ndims; d++) {
+        if (count[d] < 0 || (imap != NULL && imap[d] < 0)) { *err = NC_EINVAL; return 0; }
+        total *= count[d];
+    }
+    *n = total;
+    if (imap == NULL || ndims == 0 || total <= 1) { *span = total; return 0; }
+    d = ndims;
+    while (--d >= 0 && blk == imap[d]) blk *= count[d];
+    if (d == -1) { *span = total; return 0; }       /* contiguous layout */
+    m->ndims = ndims;
+    for (d = 0; d < ndims; d++) {
+        m->count[d] = count[d];
+        m->imap[d] = imap[d];
+        if (count[d] > m->max_count) m->max_count = count[d];
+        sp += (count[d] - 1) * imap[d];
+    }
+    *span = total ? sp + 1 : 0;
+    return 1;
+}
+
+static int launch_imap_op(const op_t *op, const void *src, void *dst, long long n, const pncxk_imap *m,
+                          int gather, int *dstatus, void *stream)
+{
+    pncxk_args a;
+    a.src = src;
+    a.dst = dst;
+    a.n = n;
+    a.fill = op->fill;
+    a.status = dstatus;
+    a.stream = stream;
+    a.nontemporal = nontemporal_mode();
+    return pncxk_launch_imap(op->kind, op->a, op->b, op->c, &a, m, gather);
+}
+
+int pncx_dev_putn_imap(int cdf_ver, int xtype, void *dxbuf, const void *dibuf, int ndims,
+                       const pncx_offset *count, const pncx_offset *imap, int itype,
+                       const void *fillp, int *dstatus, pncx_stream_t stream)
+{
+    op_t op;
+    pncxk_imap m;
+    long long n, span;
+    int err = classify(PNCX_PUT, cdf_ver, xtype, itype, fillp, &op), e2;
+    if (err != NC_NOERR) return err;
+    if (!imap_layout(ndims, count, imap, &m, &n, &span, &e2)) {
+        if (e2 != NC_NOERR) return e2;
+        return pncx_dev_putn(cdf_ver, xtype, dxbuf, dibuf, n, itype, fillp, dstatus, stream);
+    }
+    if (n <= 0) return NC_NOERR;
+    if (!have_device()) return PNCX_EDEVICE;
+    return launch_imap_op(&op, dibuf, dxbuf, n, &m, 1, dstatus, stream);
+}
+
+int pncx_dev_getn_imap(int cdf_ver, int xtype, const void *dxbuf, void *dibuf, int ndims,
+                       const pncx_offset *count, const pncx_offset *imap, int itype,
+                       int *dstatus, pncx_stream_t stream)
+{
+    op_t op;
+    pncxk_imap m;
+    long long n, span;
+    int err = classify(PNCX_GET, cdf_ver, xtype, itype, NULL, &op), e2;
+    if (err != NC_NOERR) return err;
+    if (!imap_layout(ndims, count, imap, &m, &n, &span, &e2)) {
+        if (e2 != NC_NOERR) return e2;
+        return pncx_dev_getn(cdf_ver, xtype, dxbuf, dibuf, n, itype, dstatus, stream);
+    }
+    if (n <= 0) return NC_NOERR;
+    if (!have_device()) return PNCX_EDEVICE;
+    return launch_imap_op(&op, dxbuf, dibuf, n, &m, 0, dstatus, stream);
+}
+
+/* host varm: stage the user-buffer span and the packed buffer in one slot */
+static int host_imap(int dir, int cdf_ver, int xtype, void *xbuf, void *ibuf, int ndims,
+                     const pncx_offset *count, const pncx_offset *imap, int itype, const void *fillp)
+{
+    op_t op;
+    pncxk_imap m;
+    long long n, span;
+    ctx_t *c;
+    int err = classify(dir, cdf_ver, xtype, itype, fillp, &op), e2, st = 0;
+    size_t xs, is, xb, ib;
+    uint8_t *dx, *di;
+    void *s;
+    if (err != NC_NOERR) return err;
+    if (!imap_layout(ndims, count, imap, &m, &n, &span, &e2)) {
+        if (e2 != NC_NOERR) return e2;
+        return dir == PNCX_PUT ? pncx_putn(cdf_ver, xtype, xbuf, ibuf, n, itype, fillp)
+                               : pncx_getn(cdf_ver, xtype, xbuf, ibuf, n, itype);
+    }
+    if (n <= 0) return NC_NOERR;
+    if (!have_device()) return PNCX_EDEVICE;
+    c = get_ctx();
+    if (c == NULL) return PNCX_EDEVICE;
+    xs = (size_t)pncx_xlen(xtype);
+    is = (size_t)pncx_ilen(itype);
+    xb = ALIGN16((size_t)n * xs);
+    ib = ALIGN16((size_t)span * is);
+    pthread_mutex_lock(&c->lock);
+    s = c->stream[0];
+    err = ensure_dbuf(c, xb + ib);
+    dx = (uint8_t *)c->dbuf[0];
+    di = dx + xb;
+    if (!err) err = pncxrt_memset(c->dstatus, 0, sizeof(int), s);
+    if (!err) err = pncxrt_memcpy_h2d(di, ibuf, (size_t)span * is, s);     /* user span */
+    if (dir == PNCX_PUT) {
+        if (!err && op.c) err = pncxrt_memcpy_h2d(dx, xbuf, (size_t)n * xs, s);
+        if (!err) err = launch_imap_op(&op, di, dx, n, &m, 1, c->dstatus, s);
+        if (!err) err = pncxrt_memcpy_d2h(xbuf, dx, (size_t)n * xs, s);
+    } else {
+        if (!err) err = pncxrt_memcpy_h2d(dx, xbuf, (size_t)n * xs, s);
+        if (!err) err = launch_imap_op(&op, dx, di, n, &m, 0, c->dstatus, s);
+        if (!err) err = pncxrt_memcpy_d2h(ibuf, di, (size_t)span * is, s);
+    }
+    if (!err) err = pncxrt_memcpy_d2h(&st, c->dstatus, sizeof(int), s);
+    if (!err) err = pncxrt_stream_sync(s);
+    pthread_mutex_unlock(&c->lock);
+    if (err) return err < 0 ? err : PNCX_EDEVICE;
+    return st;
+}
+
+int pncx_putn_imap(int cdf_ver, int xtype, void *xbuf, const void *ibuf, int ndims,
+                   const pncx_offset *count, const pncx_offset *imap, int itype, const void *fillp)
+{
+    return host_imap(PNCX_PUT, cdf_ver, xtype, xbuf, (void *)ibuf, ndims, count, imap, itype, fillp);
+}
+
+int pncx_getn_imap(int cdf_ver, int xtype, const void *xbuf, void *ibuf, int ndims,
+                   const pncx_offset *count, const pncx_offset *imap, int itype)
+{
+    return host_imap(PNCX_GET, cdf_ver, xtype, (void *)xbuf, ibuf, ndims, count, imap, itype, NULL);
+}
+
+/* ------------------------------------------------------------------------ */
 /* batched                                                                   */
 /* ------------------------------------------------------------------------ */
 typedef struct bitem_t {

@@ -46,6 +46,8 @@ __device__ __forceinline__ void st_unaligned(uint8_t *p, T t) {
 
 template <int A, int B> struct cmin { static constexpr int value = A < B ? A : B; };
 
+int launch_grid(int64_t work_items, int per_thread);  // defined in pncx_kern_swap.hip
+
 // ---------------------------------------------------------------------------
 // Ops
 // ---------------------------------------------------------------------------
@@ -391,6 +393,66 @@ __global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg, 
 }
 
 // ---------------------------------------------------------------------------
+// varm: the user buffer is laid out by imap[] (element strides per dimension,
+// ncmpii_create_imaptype, create_imaptype.c:25-139).  The reference packs it
+// with MPI_Pack into a contiguous cbuf and then converts (ncmpio_util.c:
+// 654-689, 716-765; unpack :842-966); here the gather (put) or scatter (get)
+// is fused with the conversion.  Packed element k (row-major over count[])
+// lives at user element offset sum_d idx_d(k) * imap[d].
+// ---------------------------------------------------------------------------
+template <typename IDX>
+__device__ __forceinline__ int64_t imap_offset(IDX k, const pncxk_imap &m) {
+    int64_t off = 0;
+#pragma unroll 1
+    for (int d = m.ndims - 1; d > 0; d--) {
+        const IDX c = (IDX)m.count[d];
+        const IDX q = k / c;
+        off += (int64_t)(k - q * c) * m.imap[d];
+        k = q;
+    }
+    return off + (int64_t)k * m.imap[0];
+}
+
+// GATHER = true: src strided (user, put); false: dst strided (user, get)
+template <class Op, bool GATHER, typename IDX>
+__global__ __launch_bounds__(256) void k_imap(const uint8_t *src, uint8_t *dst, int64_t n, pncxk_imap m,
+                                              typename Op::fill_t fill, int *status) {
+    using SU = typename Op::SU;
+    using DU = typename Op::DU;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    bool bad = false;
+    for (int64_t k = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 + threadIdx.x; k < n; k += stride) {
+        const int64_t u = imap_offset<IDX>((IDX)k, m);          // user element offset
+        const uint8_t *ps = src + (GATHER ? u : k) * Op::SS;
+        uint8_t *pd = dst + (GATHER ? k : u) * Op::DS;
+        const SU s = ld_unaligned<SU>(ps);
+        DU old = 0;
+        if constexpr (Op::PRESERVE) old = ld_unaligned<DU>(pd);
+        st_unaligned<DU>(pd, Op::one(s, old, fill, bad));
+    }
+    publish_status(status, bad);
+}
+
+template <class Op>
+int launch_imap(const pncxk_args *a, const pncxk_imap *m, int gather) {
+    if (a->n <= 0) return 0;
+    const int grid = launch_grid(a->n, 4);
+    const bool small = a->n < (1LL << 32) && m->max_count < (1LL << 32);
+    const uint8_t *src = (const uint8_t *)a->src;
+    uint8_t *dst = (uint8_t *)a->dst;
+    const typename Op::fill_t fill = (typename Op::fill_t)a->fill;
+    hipStream_t st = (hipStream_t)a->stream;
+    if (gather) {
+        if (small) hipLaunchKernelGGL((k_imap<Op, true, uint32_t>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, a->status);
+        else hipLaunchKernelGGL((k_imap<Op, true, uint64_t>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, a->status);
+    } else {
+        if (small) hipLaunchKernelGGL((k_imap<Op, false, uint32_t>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, a->status);
+        else hipLaunchKernelGGL((k_imap<Op, false, uint64_t>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, a->status);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
+}
+
+// ---------------------------------------------------------------------------
 // host-side helpers
 // ---------------------------------------------------------------------------
 // Elements before both pointers are 16B-aligned; -1 if no such split exists.
@@ -402,7 +464,6 @@ inline int64_t vec_head(const void *src, const void *dst, int64_t n) {
     return -1;
 }
 
-int launch_grid(int64_t work_items, int per_thread);  // defined in pncx_kern_swap.hip
 
 template <class Op>
 int launch_stream(const pncxk_args *a) {

@@ -43,6 +43,23 @@ extern "C" int pncxk_batch_get(int xtype, int itype, const pncxk_batch_args *a) 
     }
 }
 
+namespace {
+template <int XT, int IT>
+int get_imap(const pncxk_args *a, const pncxk_imap *m) {
+    if constexpr (same_rep<XT, IT>::value) return NC_EINVAL;
+    else return launch_imap<GetOp<XT, IT>>(a, m, 0);
+}
+}  // namespace
+
+extern "C" int pncxk_imap_get(int xtype, int itype, const pncxk_args *a, const pncxk_imap *m) {
+    switch (PNCX_KEY(xtype, itype)) {
+#define CASE(XT, IT) case PNCX_KEY(XT, IT): return get_imap<XT, IT>(a, m);
+        PNCX_ALL_PAIRS(CASE)
+#undef CASE
+        default: return NC_EBADTYPE;
+    }
+}
+
 extern "C" int pncxk_opinfo_get_get(int xtype, int itype, pncxk_opinfo *o) {
     switch (PNCX_KEY(xtype, itype)) {
 #define CASE(XT, IT) case PNCX_KEY(XT, IT): return get_info<XT, IT>(o);

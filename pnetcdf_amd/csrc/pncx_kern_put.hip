@@ -55,6 +55,28 @@ extern "C" int pncxk_batch_put(int xtype, int itype, int preserve, const pncxk_b
     }
 }
 
+namespace {
+template <int XT, int IT>
+int put_imap(int preserve, const pncxk_args *a, const pncxk_imap *m) {
+    if constexpr (same_rep<XT, IT>::value) {
+        return NC_EINVAL;
+    } else {
+        if constexpr (null_fill_preserves<XT, IT>::value)
+            if (preserve) return launch_imap<PutOp<XT, IT, true>>(a, m, 1);
+        return launch_imap<PutOp<XT, IT, false>>(a, m, 1);
+    }
+}
+}  // namespace
+
+extern "C" int pncxk_imap_put(int xtype, int itype, int preserve, const pncxk_args *a, const pncxk_imap *m) {
+    switch (PNCX_KEY(xtype, itype)) {
+#define CASE(XT, IT) case PNCX_KEY(XT, IT): return put_imap<XT, IT>(preserve, a, m);
+        PNCX_ALL_PAIRS(CASE)
+#undef CASE
+        default: return NC_EBADTYPE;
+    }
+}
+
 extern "C" int pncxk_opinfo_get_get(int xtype, int itype, pncxk_opinfo *o);
 
 extern "C" int pncxk_opinfo_getput(int kind, int xtype, int itype, int preserve, pncxk_opinfo *o) {

@@ -156,6 +156,25 @@ static __global__ __launch_bounds__(256) void k_batch_map(const pncxk_seg *segs,
     for (long long b = b0 + threadIdx.x; b < b1; b += 256) map[b] = s;
 }
 
+extern "C" int pncxk_imap_get(int xtype, int itype, const pncxk_args *a, const pncxk_imap *m);
+extern "C" int pncxk_imap_put(int xtype, int itype, int preserve, const pncxk_args *a, const pncxk_imap *m);
+
+extern "C" int pncxk_launch_imap(int kind, int a, int b, int c, const pncxk_args *args, const pncxk_imap *m,
+                          int gather) {
+    if (kind == PNCXK_SWAP) {
+        switch (a) {
+            case 1: return launch_imap<SwapOp<1>>(args, m, gather);
+            case 2: return launch_imap<SwapOp<2>>(args, m, gather);
+            case 4: return launch_imap<SwapOp<4>>(args, m, gather);
+            case 8: return launch_imap<SwapOp<8>>(args, m, gather);
+            default: return NC_EINVAL;
+        }
+    }
+    if (kind == PNCXK_GET) return pncxk_imap_get(a, b, args, m);
+    if (kind == PNCXK_PUT) return pncxk_imap_put(a, b, c, args, m);
+    return NC_EINVAL;
+}
+
 extern "C" int pncxk_batch_map(const pncxk_batch_args *a) {
     if (a->nseg <= 0 || a->dmap == nullptr) return 0;
     hipLaunchKernelGGL(k_batch_map, dim3((unsigned)a->nseg), dim3(256), 0, (hipStream_t)a->stream,

@@ -45,6 +45,16 @@ typedef struct pncxk_batch_args {
     void            *stream;
 } pncxk_batch_args;
 
+/* varm layout of the user buffer (create_imaptype.c semantics) */
+#define PNCX_MAX_DIMS 16
+typedef struct pncxk_imap {
+    int       ndims;
+    int       pad;
+    long long max_count;
+    long long count[PNCX_MAX_DIMS];
+    long long imap[PNCX_MAX_DIMS];   /* in elements of the internal type */
+} pncxk_imap;
+
 typedef struct pncxk_opinfo {
     int ss;           /* source element bytes       */
     int ds;           /* destination element bytes  */
@@ -64,6 +74,8 @@ int pncxk_swap_generic(int esize, const pncxk_args *a);  /* any esize >= 1 */
 int pncxk_get(int xtype, int itype, const pncxk_args *a);
 int pncxk_put(int xtype, int itype, int preserve, const pncxk_args *a);
 int pncxk_batch(int kind, int a, int b, int c, const pncxk_batch_args *args);
+/* fused varm gather (gather=1: put, src strided) / scatter (get, dst strided) */
+int pncxk_launch_imap(int kind, int a, int b, int c, const pncxk_args *args, const pncxk_imap *m, int gather);
 int pncxk_opinfo_get(int kind, int a, int b, int c, pncxk_opinfo *o);
 /* fill args->dmap (nblocks ints) from the device descriptors */
 int pncxk_batch_map(const pncxk_batch_args *args);

@@ -52,6 +52,10 @@ def lib():
         "pncx_dev_putn": (i, [i, i, vp, vp, ll, i, vp, vp, vp]),
         "pncx_dev_getn": (i, [i, i, vp, vp, ll, i, vp, vp]),
         "pncx_dev_batch": (i, [vp, i, vp, vp]),
+        "pncx_dev_putn_imap": (i, [i, i, vp, vp, i, vp, vp, i, vp, vp, vp]),
+        "pncx_dev_getn_imap": (i, [i, i, vp, vp, i, vp, vp, i, vp, vp]),
+        "pncx_putn_imap": (i, [i, i, vp, vp, i, vp, vp, i, vp]),
+        "pncx_getn_imap": (i, [i, i, vp, vp, i, vp, vp, i]),
         "pncx_batch": (i, [vp, i, vp]),
         "pncx_device_count": (i, []), "pncx_set_device": (i, [i]),
         "pncx_get_device": (i, []),
@@ -129,6 +133,46 @@ def getn(cdf_ver, xtype, xbuf, ibuf, nelems, itype):
     """ncmpii_getn_NC_<X>: xbuf (big-endian xtype) -> ibuf (itype)."""
     return _check(lib().pncx_getn(cdf_ver, xtype, _np_ptr(xbuf), _np_ptr(ibuf), nelems, itype),
                   "getn")
+
+
+def _offs(vals):
+    a = np.ascontiguousarray(np.asarray(vals, dtype=np.int64))
+    return a, ctypes.c_void_p(a.ctypes.data)
+
+
+def putn_imap(cdf_ver, xtype, xbuf, ibuf, count, imap, itype, fillp=None):
+    """varm put: ibuf laid out by imap[] (elements), xbuf contiguous
+    (create_imaptype.c + ncmpio_util.c:654-765, fused on the GPU)."""
+    c, cp = _offs(count)
+    m, mp = _offs(imap)
+    fb = None if fillp is None else np.frombuffer(bytes(fillp) + b"\0" * 8, np.uint8).copy()
+    return _check(lib().pncx_putn_imap(cdf_ver, xtype, _np_ptr(xbuf), _np_ptr(ibuf), len(c), cp, mp, itype,
+                                       None if fb is None else _np_ptr(fb)), "putn_imap")
+
+
+def getn_imap(cdf_ver, xtype, xbuf, ibuf, count, imap, itype):
+    c, cp = _offs(count)
+    m, mp = _offs(imap)
+    return _check(lib().pncx_getn_imap(cdf_ver, xtype, _np_ptr(xbuf), _np_ptr(ibuf), len(c), cp, mp, itype),
+                  "getn_imap")
+
+
+def dev_putn_imap(cdf_ver, xtype, dx, di, count, imap, itype, fillp=None, dstatus=None, stream=None):
+    c, cp = _offs(count)
+    m, mp = _offs(imap)
+    fb = None if fillp is None else np.frombuffer(bytes(fillp) + b"\0" * 8, np.uint8).copy()
+    _check(lib().pncx_dev_putn_imap(cdf_ver, xtype, _dptr(dx), _dptr(di), len(c), cp, mp, itype,
+                                    None if fb is None else _np_ptr(fb),
+                                    None if dstatus is None else _dptr(dstatus), _stream_ptr(stream)),
+           "dev_putn_imap", (T.NC_NOERR,))
+
+
+def dev_getn_imap(cdf_ver, xtype, dx, di, count, imap, itype, dstatus=None, stream=None):
+    c, cp = _offs(count)
+    m, mp = _offs(imap)
+    _check(lib().pncx_dev_getn_imap(cdf_ver, xtype, _dptr(dx), _dptr(di), len(c), cp, mp, itype,
+                                    None if dstatus is None else _dptr(dstatus), _stream_ptr(stream)),
+           "dev_getn_imap", (T.NC_NOERR,))
 
 
 def batch(segs):

@@ -1,0 +1,99 @@
+"""varm (imap) fused gather/scatter + conversion vs numpy gather + oracle (GPU).
+
+Reference semantics: the user buffer is addressed through imap[] (element
+strides, create_imaptype.c:25-139); MPI_Pack by that type then the
+conversion (ncmpio_util.c:654-689, 716-765), or conversion then MPI_Unpack
+(:842-966) for get.
+"""
+import numpy as np
+import pytest
+
+from pnetcdf_amd import nctypes as T
+from tests.converters import OracleConv
+
+pytestmark = pytest.mark.gpu
+
+
+def offsets(count, imap):
+    idx = np.indices(count).reshape(len(count), -1)
+    return (idx * np.asarray(imap, np.int64)[:, None]).sum(0)
+
+
+CASES = [
+    ([4, 5, 6], [1, 4, 20]),          # transposed (Fortran-order) layout
+    ([3, 7], [16, 2]),                 # padded rows, every other element
+    ([2, 3, 4], [24, 8, 1]),           # already C order (no varm): contiguous path
+    ([5, 1, 9], [100, 0, 11]),        # count 1 dim with imap 0
+    ([1000, 3], [3, 1000]),            # tall-skinny transpose
+    ([6], [5]),                        # 1-D strided
+]
+PAIRS = [(T.NC_INT, T.ITYPE_DOUBLE), (T.NC_SHORT, T.ITYPE_FLOAT), (T.NC_DOUBLE, T.ITYPE_DOUBLE),
+         (T.NC_BYTE, T.ITYPE_INT), (T.NC_UINT64, T.ITYPE_SCHAR), (T.NC_FLOAT, T.ITYPE_FLOAT)]
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+@pytest.mark.parametrize("count,imap", CASES)
+@pytest.mark.parametrize("xt,it", PAIRS)
+@pytest.mark.parametrize("where", ["host", "dev"])
+def test_imap_put_get(torch_cuda, count, imap, xt, it, where):
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    ora = OracleConv()
+    rng = np.random.default_rng(sum(count) + xt * 11 + it)
+    off = offsets(count, imap)
+    n = off.size
+    span = int(off.max()) + 1 if n else 0
+    user = np.frombuffer(rng.integers(0, 256, span * T.ilen(it) + 8, dtype=np.uint8).tobytes(),
+                         T.ITYPE_NP[it])[:span].copy()
+    if np.issubdtype(user.dtype, np.floating):
+        user = rng.standard_normal(span).astype(user.dtype) * 1e4
+    fill = T.fill_bytes(xt, 42)
+    # ---- put: gather + convert
+    exp_x, exp_st = ora.putn(5, xt, user[off], it, fill)
+    if where == "host":
+        xb = np.zeros(n * T.xlen(xt), np.uint8)
+        st = pncx.putn_imap(5, xt, xb, user, count, imap, it, fill)
+        got_x = xb.tobytes()
+    else:
+        du = torch.from_numpy(user.view(np.uint8).copy()).cuda()
+        dx = torch.zeros(max(n * T.xlen(xt), 16), dtype=torch.uint8, device="cuda")
+        ds = torch.zeros(1, dtype=torch.int32, device="cuda")
+        pncx.dev_putn_imap(5, xt, dx, du, count, imap, it, fill, ds)
+        torch.cuda.synchronize()
+        got_x, st = dx.cpu().numpy()[:n * T.xlen(xt)].tobytes(), int(ds.item())
+    assert st == exp_st and got_x == exp_x
+    # ---- get: convert + scatter (untouched user elements must survive)
+    vals, gst = ora.getn(5, xt, exp_x, it)
+    exp_user = user.copy()
+    exp_user[off] = vals
+    if where == "host":
+        out = user.copy()
+        st = pncx.getn_imap(5, xt, np.frombuffer(exp_x, np.uint8).copy(), out, count, imap, it)
+    else:
+        du = torch.from_numpy(user.view(np.uint8).copy()).cuda()
+        dx = torch.from_numpy(np.frombuffer(exp_x + b"\0" * 16, np.uint8).copy()).cuda()
+        ds = torch.zeros(1, dtype=torch.int32, device="cuda")
+        pncx.dev_getn_imap(5, xt, dx, du, count, imap, it, ds)
+        torch.cuda.synchronize()
+        out = np.frombuffer(du.cpu().numpy().tobytes(), user.dtype)
+        st = int(ds.item())
+    assert st == gst
+    assert out.tobytes() == exp_user.tobytes()
+
+
+def test_imap_rejects_bad_args(torch_cuda):
+    from pnetcdf_amd import pncx
+    xb = np.zeros(64, np.uint8)
+    ib = np.zeros(64, np.uint8)
+    import ctypes
+    lib = pncx.lib()
+    cnt = (ctypes.c_longlong * 2)(2, -1)
+    imp = (ctypes.c_longlong * 2)(1, 1)
+    assert lib.pncx_putn_imap(5, T.NC_INT, xb.ctypes.data, ib.ctypes.data, 2, cnt, imp, T.ITYPE_INT, None) == T.NC_EINVAL
+    assert lib.pncx_putn_imap(5, T.NC_INT, xb.ctypes.data, ib.ctypes.data, 17, cnt, imp, T.ITYPE_INT, None) == T.NC_EINVAL
