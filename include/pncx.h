@@ -185,6 +185,16 @@ int pncx_dev_getn(int cdf_ver, int xtype, const void *dxbuf, void *dibuf,
                   pncx_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
+/* Fill path: fill_var_buf (src/drivers/ncmpio/ncmpio_fill.c:89-140).         */
+/* Replicates one external (big-endian) fill value of xtype over nelems      */
+/* elements.  xvalue = the _FillValue attribute's external bytes, or NULL    */
+/* for the default NC_FILL_<X> pattern (ncmpio_fill.c:50-60).                */
+/* ------------------------------------------------------------------------ */
+int pncx_dev_fill(int xtype, void *dxbuf, pncx_offset nelems, const void *xvalue,
+                  pncx_stream_t stream);
+int pncx_fill(int xtype, void *xbuf, pncx_offset nelems, const void *xvalue);
+
+/* ------------------------------------------------------------------------ */
 /* varm: internal buffer laid out by imap[] (element strides per dimension,  */
 /* ncmpii_create_imaptype, src/drivers/common/create_imaptype.c:25-139),     */
 /* external buffer contiguous row-major over count[].  Replaces the MPI_Pack */

@@ -424,6 +424,81 @@ int pncx_getn(int cdf_ver, int xtype, const void *xbuf, void *ibuf, pncx_offset 
 }
 
 /* ------------------------------------------------------------------------ */
+/* fill path: fill_var_buf (ncmpio_fill.c:89-140)                            */
+/* ------------------------------------------------------------------------ */
+/* default external fill patterns, big-endian (ncmpio_fill.c:50-60) */
+static int default_fill_xvalue(int xtype, unsigned char *out)
+{
+    static const unsigned char f_char[1] = {0x00}, f_byte[1] = {0x81}, f_short[2] = {0x80, 0x01},
+        f_int[4] = {0x80, 0x00, 0x00, 0x01}, f_float[4] = {0x7C, 0xF0, 0x00, 0x00},
+        f_double[8] = {0x47, 0x9E, 0, 0, 0, 0, 0, 0}, f_ubyte[1] = {0xFF}, f_ushort[2] = {0xFF, 0xFF},
+        f_uint[4] = {0xFF, 0xFF, 0xFF, 0xFF}, f_int64[8] = {0x80, 0, 0, 0, 0, 0, 0, 0x02},
+        f_uint64[8] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFE};
+    const unsigned char *p;
+    switch (xtype) {
+        case NC_CHAR: p = f_char; break;
+        case NC_BYTE: p = f_byte; break;
+        case NC_SHORT: p = f_short; break;
+        case NC_INT: p = f_int; break;
+        case NC_FLOAT: p = f_float; break;
+        case NC_DOUBLE: p = f_double; break;
+        case NC_UBYTE: p = f_ubyte; break;
+        case NC_USHORT: p = f_ushort; break;
+        case NC_UINT: p = f_uint; break;
+        case NC_INT64: p = f_int64; break;
+        case NC_UINT64: p = f_uint64; break;
+        default: return NC_EBADTYPE;
+    }
+    memcpy(out, p, (size_t)pncx_xlen(xtype));
+    return NC_NOERR;
+}
+
+int pncx_dev_fill(int xtype, void *dxbuf, pncx_offset nelems, const void *xvalue, pncx_stream_t stream)
+{
+    unsigned char v[8];
+    const int xs = pncx_xlen(xtype);
+    if (xs < 0) return NC_EBADTYPE;
+    if (xvalue == NULL) {
+        if (default_fill_xvalue(xtype, v) != NC_NOERR) return NC_EBADTYPE;
+    } else {
+        memcpy(v, xvalue, (size_t)xs);
+    }
+    if (nelems <= 0) return NC_NOERR;
+    if (!have_device()) return PNCX_EDEVICE;
+    return pncxk_fill(dxbuf, nelems, xs, v, stream);
+}
+
+int pncx_fill(int xtype, void *xbuf, pncx_offset nelems, const void *xvalue)
+{
+    ctx_t *c;
+    long long off, chunk;
+    int err = 0, slot = 0, i;
+    const int xs = pncx_xlen(xtype);
+    if (xs < 0) return NC_EBADTYPE;
+    if (nelems <= 0) return NC_NOERR;
+    if (!have_device()) return PNCX_EDEVICE;
+    c = get_ctx();
+    if (c == NULL) return PNCX_EDEVICE;
+    pthread_mutex_lock(&c->lock);
+    chunk = (long long)(chunk_bytes() / (size_t)xs);
+    if (chunk > nelems) chunk = nelems;
+    err = ensure_dbuf(c, ALIGN16((size_t)chunk * xs));
+    /* the pattern is generated once per slot and streamed out chunk by chunk */
+    for (i = 0; i < NSLOT && !err; i++)
+        err = pncx_dev_fill(xtype, c->dbuf[i], chunk, xvalue, c->stream[i]);
+    for (off = 0; off < nelems && !err; off += chunk, slot ^= 1) {
+        const long long m = nelems - off < chunk ? nelems - off : chunk;
+        err = pncxrt_memcpy_d2h((uint8_t *)xbuf + (size_t)off * xs, c->dbuf[slot], (size_t)m * xs, c->stream[slot]);
+    }
+    for (i = 0; i < NSLOT; i++) {
+        int e2 = pncxrt_stream_sync(c->stream[i]);
+        if (!err && e2) err = e2;
+    }
+    pthread_mutex_unlock(&c->lock);
+    return err ? (err < 0 ? err : PNCX_EDEVICE) : NC_NOERR;
+}
+
+/* ------------------------------------------------------------------------ */
 /* varm (imap) fused gather/scatter + conversion                             */
 /* ------------------------------------------------------------------------ */
 /* Mirrors ncmpii_create_imaptype (create_imaptype.c:25-139): returns 1 with

@@ -84,6 +84,48 @@ extern "C" int pncxk_swap_generic(int esize, const pncxk_args *a) {
     return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
 }
 
+// ---------------------------------------------------------------------------
+// fill_var_buf (ncmpio_fill.c:89-140): replicate one xsize-byte external
+// (big-endian) fill value over the buffer.  Pure write: one-shot grid, one
+// nontemporal 16 B store per lane (16 is a multiple of every xsize), scalar
+// bytes before the first 16 B boundary and after the last.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fill(uint8_t *dst, int64_t nbytes, int64_t head, int64_t nvec,
+                                              u32x4 pattern, uint64_t xvalue, int xsize) {
+    const int64_t nb = gridDim.x;
+    if (blockIdx.x == 0) {
+        const int64_t tail0 = head + nvec * 16;
+        for (int64_t j = threadIdx.x; j < head; j += 256) dst[j] = (uint8_t)(xvalue >> (8 * (j % xsize)));
+        for (int64_t j = tail0 + threadIdx.x; j < nbytes; j += 256)
+            dst[j] = (uint8_t)(xvalue >> (8 * (j % xsize)));
+    }
+    u32x4 *v = reinterpret_cast<u32x4 *>(dst + head);
+    for (int64_t k = xcd_remap(blockIdx.x, nb) * 256 + threadIdx.x; k < nvec; k += nb * 256)
+        __builtin_nontemporal_store(pattern, v + k);
+}
+
+extern "C" int pncxk_fill(void *dst, long long nelems, int xsize, const void *xvalue, void *stream) {
+    if (nelems <= 0) return 0;
+    if (xsize != 1 && xsize != 2 && xsize != 4 && xsize != 8) return NC_EINVAL;
+    uint64_t xv = 0;
+    memcpy(&xv, xvalue, (size_t)xsize);                  // external bytes, in memory order
+    const int64_t nbytes = (int64_t)nelems * xsize;
+    const uintptr_t a = (uintptr_t)dst;
+    int64_t head = (int64_t)((16 - (a & 15)) & 15);
+    if (head > nbytes) head = nbytes;
+    const int64_t nvec = (nbytes - head) / 16;
+    uint8_t pb[16];
+    for (int b = 0; b < 16; b++) pb[b] = (uint8_t)(xv >> (8 * ((head + b) % xsize)));
+    u32x4 pattern;
+    memcpy(&pattern, pb, 16);
+    int64_t grid = (nvec + 255) / 256;
+    if (grid < 1) grid = 1;
+    if (grid > MAX_BLOCKS) grid = MAX_BLOCKS;
+    hipLaunchKernelGGL(k_fill, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, (uint8_t *)dst, nbytes,
+                       head, nvec, pattern, xv, xsize);
+    return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
+}
+
 // batch / opinfo dispatch: get and put live in their own TUs
 extern "C" int pncxk_batch_get(int xtype, int itype, const pncxk_batch_args *a);
 extern "C" int pncxk_batch_put(int xtype, int itype, int preserve, const pncxk_batch_args *a);

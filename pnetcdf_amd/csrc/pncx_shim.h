@@ -77,6 +77,8 @@ int pncxk_batch(int kind, int a, int b, int c, const pncxk_batch_args *args);
 /* fused varm gather (gather=1: put, src strided) / scatter (get, dst strided) */
 int pncxk_launch_imap(int kind, int a, int b, int c, const pncxk_args *args, const pncxk_imap *m, int gather);
 int pncxk_opinfo_get(int kind, int a, int b, int c, pncxk_opinfo *o);
+/* replicate an xsize-byte external value over nelems elements (device) */
+int pncxk_fill(void *dst, long long nelems, int xsize, const void *xvalue, void *stream);
 /* fill args->dmap (nblocks ints) from the device descriptors */
 int pncxk_batch_map(const pncxk_batch_args *args);
 

@@ -57,6 +57,8 @@ def lib():
         "pncx_putn_imap": (i, [i, i, vp, vp, i, vp, vp, i, vp]),
         "pncx_getn_imap": (i, [i, i, vp, vp, i, vp, vp, i]),
         "pncx_batch": (i, [vp, i, vp]),
+        "pncx_dev_fill": (i, [i, vp, ll, vp, vp]),
+        "pncx_fill": (i, [i, vp, ll, vp]),
         "pncx_device_count": (i, []), "pncx_set_device": (i, [i]),
         "pncx_get_device": (i, []),
         "pncx_dev_status_read": (i, [vp, vp]),
@@ -133,6 +135,20 @@ def getn(cdf_ver, xtype, xbuf, ibuf, nelems, itype):
     """ncmpii_getn_NC_<X>: xbuf (big-endian xtype) -> ibuf (itype)."""
     return _check(lib().pncx_getn(cdf_ver, xtype, _np_ptr(xbuf), _np_ptr(ibuf), nelems, itype),
                   "getn")
+
+
+def fill(xtype, xbuf, nelems, xvalue=None):
+    """fill_var_buf (ncmpio_fill.c:89-140) into a host buffer; xvalue = the
+    external (big-endian) bytes of a _FillValue, None for the default."""
+    xv = None if xvalue is None else np.frombuffer(bytes(xvalue) + b"\0" * 8, np.uint8).copy()
+    _check(lib().pncx_fill(xtype, _np_ptr(xbuf), nelems, None if xv is None else _np_ptr(xv)), "fill",
+           (T.NC_NOERR,))
+
+
+def dev_fill(xtype, dx, nelems, xvalue=None, stream=None):
+    xv = None if xvalue is None else np.frombuffer(bytes(xvalue) + b"\0" * 8, np.uint8).copy()
+    _check(lib().pncx_dev_fill(xtype, _dptr(dx), nelems, None if xv is None else _np_ptr(xv),
+                               _stream_ptr(stream)), "dev_fill", (T.NC_NOERR,))
 
 
 def _offs(vals):
