@@ -248,6 +248,14 @@ int pncx_batch(const pncx_seg *segs, int nseg, int *status_out);
 int  pncx_device_count(void);
 int  pncx_set_device(int dev);
 int  pncx_get_device(void);
+/* Pin a long-lived host buffer for direct DMA (no reference equivalent: the
+ * xbuf of ncmpio_getput.m4:216,422 is malloc'ed per call).  Host entry points
+ * pin buffers >= 64 MiB themselves for the duration of a call; a buffer
+ * registered here skips that per-call cost (~30 ms per 4 GiB on MI355X
+ * hosts).  Returns NC_NOERR, also when the range is already pinned, or
+ * PNCX_EDEVICE.  Unregister before freeing the memory. */
+int  pncx_host_register(void *buf, pncx_offset nbytes);
+int  pncx_host_unregister(void *buf);
 /* Synchronise `stream` and return *dstatus (NC_NOERR if it was 0). */
 int  pncx_dev_status_read(const int *dstatus, pncx_stream_t stream);
 const char *pncx_strerror(int err);

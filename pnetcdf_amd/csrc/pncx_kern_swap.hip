@@ -296,6 +296,19 @@ int pncxrt_event_sync(void *e) { return rt(hipEventSynchronize((hipEvent_t)e), "
 int pncxrt_event_elapsed_ms(float *ms, void *a, void *b) {
     return rt(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b), "hipEventElapsedTime");
 }
+int pncxrt_host_register(void *p, size_t n) {
+    /* hipHostRegister on an already registered range returns success and a
+     * later unregister would drop the owner's registration: look first */
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) == hipSuccess &&
+        (at.type == hipMemoryTypeHost || at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged))
+        return 1;
+    (void)hipGetLastError();
+    if (hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess) return 0;
+    (void)hipGetLastError();
+    return PNCX_EDEVICE;
+}
+int pncxrt_host_unregister(void *p) { return rt(hipHostUnregister(p), "hipHostUnregister"); }
 int pncxrt_is_device_ptr(const void *p) {
     hipPointerAttribute_t at;
     if (hipPointerGetAttributes(&at, p) != hipSuccess) {

@@ -104,6 +104,10 @@ int  pncxrt_stream_wait_event(void *stream, void *e);
 int  pncxrt_event_sync(void *e);
 int  pncxrt_event_elapsed_ms(float *ms, void *start, void *stop);
 int  pncxrt_is_device_ptr(const void *p);
+/* pin a pageable host range for DMA: 0 = registered by this call (caller
+ * unregisters), 1 = already pinned/registered, PNCX_EDEVICE = could not */
+int  pncxrt_host_register(void *p, size_t n);
+int  pncxrt_host_unregister(void *p);
 const char *pncxrt_last_error(void);
 
 #ifdef __cplusplus

@@ -61,6 +61,7 @@ def lib():
         "pncx_fill": (i, [i, vp, ll, vp]),
         "pncx_device_count": (i, []), "pncx_set_device": (i, [i]),
         "pncx_get_device": (i, []),
+        "pncx_host_register": (i, [vp, ll]), "pncx_host_unregister": (i, [vp]),
         "pncx_dev_status_read": (i, [vp, vp]),
         "pncx_strerror": (ctypes.c_char_p, [i]),
         "pncx_version": (ctypes.c_char_p, []),
@@ -93,6 +94,15 @@ class Seg(ctypes.Structure):
     _fields_ = [("dir", ctypes.c_int), ("cdf_ver", ctypes.c_int), ("xtype", ctypes.c_int),
                 ("itype", ctypes.c_int), ("nelems", ctypes.c_longlong),
                 ("xbuf", ctypes.c_void_p), ("ibuf", ctypes.c_void_p), ("fillp", ctypes.c_void_p)]
+
+
+def host_register(buf):
+    """Pin a long-lived host numpy buffer for direct DMA (pncx_host_register)."""
+    _check(lib().pncx_host_register(_np_ptr(buf), buf.nbytes), "host_register", (T.NC_NOERR,))
+
+
+def host_unregister(buf):
+    _check(lib().pncx_host_unregister(_np_ptr(buf)), "host_unregister", (T.NC_NOERR,))
 
 
 def _np_ptr(a):

@@ -126,6 +126,47 @@ def test_host_in_swapn(torch_cuda, esize, n):
     assert np.array_equal(buf, ref)
 
 
+@pytest.mark.parametrize("kind", ["pageable", "pageable_unaligned", "torch_pinned", "registered"])
+def test_host_large_pinned_paths(torch_cuda, kind):
+    """Host buffers >= 64 MiB are pinned for the call (hipHostRegister) and
+    unpinned after; already-pinned buffers are used as they are.  Multi-chunk
+    sizes, repeated calls (register/unregister cycles), swap + getn + putn."""
+    from pnetcdf_amd import pncx
+    n = (96 << 20) // 8 + 5
+    rng = np.random.default_rng(0x9127)
+    if kind == "torch_pinned":
+        raw = torch_cuda.empty(n * 8 + 16, dtype=torch_cuda.uint8, pin_memory=True).numpy()
+        raw[:] = rng.integers(0, 256, raw.size, dtype=np.uint8)
+        buf = raw[:n * 8]
+    else:
+        raw = rng.integers(0, 256, n * 8 + 16, dtype=np.uint8)
+        buf = raw[3:3 + n * 8] if kind == "pageable_unaligned" else raw[:n * 8]
+    if kind == "registered":
+        pncx.host_register(raw)
+        pncx.host_register(raw)          # already pinned: still NC_NOERR
+    orig = buf.copy()
+    for _ in range(2):
+        pncx.in_swapn(buf, n, 8)
+        assert np.array_equal(buf.view(np.uint8).reshape(-1, 8), orig.reshape(-1, 8)[:, ::-1])
+        pncx.in_swapn(buf, n, 8)
+        assert np.array_equal(buf, orig)
+    # NC_INT (big-endian) -> double, then double -> NC_INT with ERANGE fill
+    m = buf.size // 4
+    out = np.empty(m, np.float64)
+    st = pncx.getn(5, T.NC_INT, buf, out, m, T.ITYPE_DOUBLE)
+    assert st == T.NC_NOERR
+    assert np.array_equal(out, np.frombuffer(buf.tobytes(), ">i4").astype(np.float64))
+    out[::1000] = 1e300
+    xb = np.empty(m * 4, np.uint8)
+    st = pncx.putn(5, T.NC_INT, xb, out, m, T.ITYPE_DOUBLE, T.fill_bytes(T.NC_INT))
+    assert st == T.NC_ERANGE
+    exp = np.frombuffer(buf.tobytes(), ">i4").copy()
+    exp[::1000] = T.XTYPE_FILL[T.NC_INT]
+    assert np.array_equal(np.frombuffer(xb.tobytes(), ">i4"), exp)
+    if kind == "registered":
+        pncx.host_unregister(raw)
+
+
 @pytest.mark.parametrize("esize", [2, 4, 8])
 @pytest.mark.parametrize("offset", [0, 1, 2, 4, 8, 12])
 def test_dev_swap_offsets(torch_cuda, esize, offset):

@@ -18,7 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def timeit(fn, reps=3):
+def timeit(fn, reps=5):
+    """median of `reps` timed calls after one warm call"""
     fn()
     ts = []
     for _ in range(reps):
@@ -50,6 +51,11 @@ def main():
     pp = ctypes.c_void_p(pin.data_ptr())
     t = timeit(lambda: lib.pncx_in_swapn(pp, n8, 8))
     res["in_swapn8_host_pinned"] = {"s": t, "slab_GiBps": nbytes / t / GIB, "moved_GiBps": 2 * nbytes / t / GIB}
+    # pageable buffer registered once by the application (pncx_host_register)
+    pncx.host_register(buf)
+    t = timeit(lambda: lib.pncx_in_swapn(p, n8, 8))
+    res["in_swapn8_host_registered"] = {"s": t, "slab_GiBps": nbytes / t / GIB, "moved_GiBps": 2 * nbytes / t / GIB}
+    pncx.host_unregister(buf)
     # config-3 shape from host buffers: NC_INT -> double
     n4 = nbytes // 8          # ints (xbuf = nbytes/2, ibuf = nbytes)
     xb = np.frombuffer(np.random.default_rng(3).bytes(n4 * 4), np.uint8).copy()
@@ -57,6 +63,13 @@ def main():
     t = timeit(lambda: lib.pncx_getn(5, T.NC_INT, ctypes.c_void_p(xb.ctypes.data), ctypes.c_void_p(ib.ctypes.data),
                                      n4, T.ITYPE_DOUBLE))
     res["getn_int_double_host"] = {"s": t, "moved_GiBps": 12 * n4 / t / GIB}
+    pncx.host_register(xb)
+    pncx.host_register(ib)
+    t = timeit(lambda: lib.pncx_getn(5, T.NC_INT, ctypes.c_void_p(xb.ctypes.data), ctypes.c_void_p(ib.ctypes.data),
+                                     n4, T.ITYPE_DOUBLE))
+    res["getn_int_double_host_registered"] = {"s": t, "moved_GiBps": 12 * n4 / t / GIB}
+    pncx.host_unregister(xb)
+    pncx.host_unregister(ib)
     # CPU oracle, 1 thread, same buffers
     t = timeit(lambda: O.lib().orc_in_swapn(p, n8, 8), reps=2)
     res["cpu_oracle_in_swapn8_1core"] = {"s": t, "moved_GiBps": 2 * nbytes / t / GIB}
