@@ -47,6 +47,14 @@ def test_pncx_h_symbols_exported(built):
     assert not missing, missing
 
 
+def test_pncx_nc_h_symbols_exported(built):
+    """file-level API (include/pncx_nc.h)"""
+    decl = declared("pncx_nc.h")
+    assert len(decl) == 44
+    missing = [s for s in decl if s not in exported(LIB)]
+    assert not missing, missing
+
+
 def test_ncmpii_symbols_exported(built):
     decl = declared("pncx_ncmpii.h")
     # the 22 conversion symbols of common.h:147-221 (+ CHAR put/get, mapper)
