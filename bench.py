@@ -65,6 +65,37 @@ def cpu_baseline_swap8(budget_s=12.0, slab_bytes=2 << 30):
                       f"in {el:.1f} s (oracle/pncx_oracle.c orc_in_swapn, gcc -O2, 1 thread)"}
 
 
+def cpu_baseline_swap8_threads(budget_s=4.0, slab_bytes=2 << 30, threads=None):
+    """Same restatement on all host cores the box gives one GPU (16): one
+    thread per disjoint slice of the slab, the N-ranks-per-node picture of
+    BASELINE.md §3.  ctypes releases the GIL during the C call."""
+    import threading
+    from oracle import oracle as O
+    lib = O.lib()
+    nt = threads or min(16, os.cpu_count() or 1)
+    buf = np.frombuffer(np.random.default_rng(SEEDS["c2"]).bytes(slab_bytes), dtype=np.uint64).copy()
+    per = buf.size // nt
+    passes = [0] * nt
+    t_end = time.perf_counter() + budget_s
+
+    def work(k):
+        ptr = ctypes.c_void_p(buf[k * per:].ctypes.data)
+        while time.perf_counter() < t_end:
+            lib.orc_in_swapn(ptr, per, 8)
+            passes[k] += 1
+    ths = [threading.Thread(target=work, args=(k,)) for k in range(nt)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    el = time.perf_counter() - t0
+    moved = 16.0 * per * sum(passes)
+    return {"value": round(moved / el / GIB, 3), "unit": "GiB/s", "cores": nt, "kind": "port",
+            "sample": f"{slab_bytes >> 30} GiB slab split over {nt} threads, {sum(passes)} slice passes "
+                      f"in {el:.1f} s (orc_in_swapn, gcc -O2)"}
+
+
 def load_traffic(kernel_key, elems_per_launch):
     """HBM traffic per launch from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, tools/pmc_summary.py; FETCH_SIZE doubled per
@@ -212,9 +243,10 @@ def main():
     traffic = load_traffic(metric_key, elems)
 
     if rank == 0:
-        cpu = None
+        cpu = cpu_all = None
         if world == 1 and not args.no_cpu_baseline and args.workload == "c2":
             cpu = cpu_baseline_swap8(args.cpu_budget)
+            cpu_all = cpu_baseline_swap8_threads()
         line = {
             "metric": "GiB/s device-resident swap+type-convert, 2/4/8-byte NC arrays",
             "value": round(value, 2),
@@ -235,6 +267,7 @@ def main():
                          "kernel_ms_avg": round(kern_ms, 4),
                          "algorithmic_bytes_per_launch": bytes_per_elem * elems},
             "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_all,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

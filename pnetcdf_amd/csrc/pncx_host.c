@@ -277,6 +277,9 @@ typedef struct ctx_t {
     void  *hscratch;          /* pinned host mirror of dscratch */
     size_t hscratch_size;
     pthread_mutex_t lock;
+    void  *barena;            /* device arena of pncx_batch, kept across calls */
+    size_t barena_size;
+    pthread_mutex_t block;
 } ctx_t;
 
 static ctx_t g_ctx[MAX_DEV];
@@ -305,6 +308,7 @@ static ctx_t *get_ctx(void)
         int err = 0;
         memset(c, 0, sizeof *c);
         pthread_mutex_init(&c->lock, NULL);
+        pthread_mutex_init(&c->block, NULL);
         for (i = 0; i < NSLOT && !err; i++) err = pncxrt_stream_create(&c->stream[i]);
         if (!err) err = pncxrt_malloc((void **)&c->dstatus, NSLOT * sizeof(int));
         if (err) {
@@ -956,7 +960,20 @@ int pncx_batch(const pncx_seg *segs, int nseg, int *status_out)
         if (xs < 0 || is < 0 || segs[i].nelems <= 0) continue;
         total += ALIGN16((size_t)segs[i].nelems * xs) + ALIGN16((size_t)segs[i].nelems * is);
     }
-    if (pncxrt_malloc((void **)&arena, total ? total : 16) != 0) { free(dsegs); return PNCX_EDEVICE; }
+    if (total == 0) total = 16;
+    pthread_mutex_lock(&c->block);
+    if (c->barena_size < total) {           /* grow-only: hipMalloc per call costs more than the batch */
+        if (c->barena) pncxrt_free(c->barena);
+        c->barena = NULL;
+        c->barena_size = 0;
+        if (pncxrt_malloc(&c->barena, total) != 0) {
+            pthread_mutex_unlock(&c->block);
+            free(dsegs);
+            return PNCX_EDEVICE;
+        }
+        c->barena_size = total;
+    }
+    arena = (uint8_t *)c->barena;
     for (i = 0; i < nseg && !err; i++) {
         const pncx_seg *s = &segs[i];
         const int xs = pncx_xlen(s->xtype), is = pncx_ilen(s->itype);
@@ -985,7 +1002,7 @@ int pncx_batch(const pncx_seg *segs, int nseg, int *status_out)
             err = pncxrt_memcpy_d2h(s->ibuf, dsegs[i].ibuf, (size_t)s->nelems * is, c->stream[0]);
     }
     if (!err) err = pncxrt_stream_sync(c->stream[0]);
-    pncxrt_free(arena);
+    pthread_mutex_unlock(&c->block);
     free(dsegs);
     if (err) return PNCX_EDEVICE;
     return ret;

@@ -1,0 +1,232 @@
+/*
+ * pncx_io.c -- parallel POSIX I/O pool (see pncx_io.h).
+ *
+ * The reference hands the packed buffer to MPI-IO (ncmpio_file_io.c); for one
+ * process on a node-local file system the cost is the page-cache copy, which
+ * one thread does at a few GB/s.  Splitting the copy over the host cores the
+ * box gives a GPU (PNCX_IO_THREADS, default 8) raises that, and running it
+ * asynchronously lets it overlap the GPU conversion of the next chunk.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include "pncx.h"
+#include "pncx_nc.h"
+#include "pncx_io.h"
+
+#define MAX_THREADS 64
+#define INLINE_BYTES (1u << 20)      /* below this a job runs in the caller */
+#define MIN_TASK_BYTES (1u << 20)    /* no task smaller than this */
+
+typedef struct task {
+    struct task *next;
+    pio_batch *b;
+    int fd, write;
+    pio_run *runs;                   /* shared by the tasks of one job */
+    size_t n;
+    long long lo, hi;                /* byte range of the concatenated runs */
+    int *refs;                       /* tasks still using runs[] */
+} task;
+
+static pthread_mutex_t q_lock = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t q_cond = PTHREAD_COND_INITIALIZER;
+static task *q_head, *q_tail;
+static int n_threads = -1;
+
+int pio_write_all(int fd, const void *buf, size_t n, long long off)
+{
+    const char *p = (const char *)buf;
+    while (n > 0) {
+        const size_t m = n > (1u << 30) ? (1u << 30) : n;
+        const ssize_t w = pwrite(fd, p, m, (off_t)off);
+        if (w < 0) { if (errno == EINTR) continue; return NC_EWRITE; }
+        if (w == 0) return NC_EWRITE;
+        p += w; n -= (size_t)w; off += w;
+    }
+    return NC_NOERR;
+}
+
+/* reads past the end of file return zeros (never-written data) */
+int pio_read_all(int fd, void *buf, size_t n, long long off)
+{
+    char *p = (char *)buf;
+    while (n > 0) {
+        const size_t m = n > (1u << 30) ? (1u << 30) : n;
+        const ssize_t r = pread(fd, p, m, (off_t)off);
+        if (r < 0) { if (errno == EINTR) continue; return NC_EREAD; }
+        if (r == 0) { memset(p, 0, n); return NC_NOERR; }
+        p += r; n -= (size_t)r; off += r;
+    }
+    return NC_NOERR;
+}
+
+/* copy bytes [lo, hi) of the concatenation of runs */
+static int do_range(int fd, int write, const pio_run *runs, size_t n, long long lo, long long hi)
+{
+    long long pos = 0;
+    size_t i;
+    int err = NC_NOERR;
+    for (i = 0; i < n && pos < hi && !err; i++) {
+        const long long a = pos, b = pos + runs[i].len;
+        pos = b;
+        if (b <= lo) continue;
+        {
+            const long long s = a > lo ? a : lo, e = b < hi ? b : hi;
+            const long long k = s - a;
+            err = write ? pio_write_all(fd, runs[i].mem + k, (size_t)(e - s), runs[i].off + k)
+                        : pio_read_all(fd, runs[i].mem + k, (size_t)(e - s), runs[i].off + k);
+        }
+    }
+    return err;
+}
+
+/* one share of a job is done: record its error, release the shared runs */
+static void share_done(pio_batch *b, pio_run *runs, int *refs, int err)
+{
+    int last;
+    pthread_mutex_lock(&b->m);
+    if (err && !b->err) b->err = err;
+    b->pending--;
+    if (b->pending == 0) pthread_cond_broadcast(&b->c);
+    pthread_mutex_unlock(&b->m);
+    pthread_mutex_lock(&q_lock);
+    last = --(*refs) == 0;
+    pthread_mutex_unlock(&q_lock);
+    if (last) { free(runs); free(refs); }
+}
+
+static void finish(task *t, int err)
+{
+    share_done(t->b, t->runs, t->refs, err);
+    free(t);
+}
+
+static void *worker(void *arg)
+{
+    (void)arg;
+    for (;;) {
+        task *t;
+        pthread_mutex_lock(&q_lock);
+        while (q_head == NULL) pthread_cond_wait(&q_cond, &q_lock);
+        t = q_head;
+        q_head = t->next;
+        if (q_head == NULL) q_tail = NULL;
+        pthread_mutex_unlock(&q_lock);
+        finish(t, do_range(t->fd, t->write, t->runs, t->n, t->lo, t->hi));
+    }
+    return NULL;
+}
+
+int pio_threads(void)
+{
+    pthread_mutex_lock(&q_lock);
+    if (n_threads < 0) {
+        const char *e = getenv("PNCX_IO_THREADS");
+        int n = e ? atoi(e) : 8, i;
+        if (n < 1) n = 1;
+        if (n > MAX_THREADS) n = MAX_THREADS;
+        n_threads = 0;
+        for (i = 0; i < n; i++) {
+            pthread_t th;
+            pthread_attr_t at;
+            pthread_attr_init(&at);
+            pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
+            if (pthread_create(&th, &at, worker, NULL) == 0) n_threads++;
+            pthread_attr_destroy(&at);
+        }
+    }
+    pthread_mutex_unlock(&q_lock);
+    return n_threads;
+}
+
+void pio_batch_init(pio_batch *b)
+{
+    pthread_mutex_init(&b->m, NULL);
+    pthread_cond_init(&b->c, NULL);
+    b->pending = 0;
+    b->err = NC_NOERR;
+}
+
+void pio_batch_destroy(pio_batch *b)
+{
+    pthread_mutex_destroy(&b->m);
+    pthread_cond_destroy(&b->c);
+}
+
+int pio_submit(pio_batch *b, int fd, int write, const pio_run *runs, size_t n)
+{
+    long long total = 0, per;
+    size_t i;
+    int nt, k, *refs;
+    pio_run *copy;
+    for (i = 0; i < n; i++) total += runs[i].len;
+    if (total == 0) return NC_NOERR;
+    nt = total < INLINE_BYTES ? 0 : pio_threads();
+    if (nt <= 1) {
+        const int err = do_range(fd, write, runs, n, 0, total);
+        if (err) {
+            pthread_mutex_lock(&b->m);
+            if (!b->err) b->err = err;
+            pthread_mutex_unlock(&b->m);
+        }
+        return err;
+    }
+    if ((long long)nt * MIN_TASK_BYTES > total) nt = (int)(total / MIN_TASK_BYTES);
+    if (nt < 1) nt = 1;
+    copy = (pio_run *)malloc(sizeof(pio_run) * n);
+    refs = (int *)malloc(sizeof(int));
+    if (copy == NULL || refs == NULL) { free(copy); free(refs); return NC_ENOMEM; }
+    memcpy(copy, runs, sizeof(pio_run) * n);
+    *refs = nt;
+    per = (total + nt - 1) / nt;
+    pthread_mutex_lock(&b->m);
+    b->pending += nt;
+    pthread_mutex_unlock(&b->m);
+    for (k = 0; k < nt; k++) {
+        task *t = (task *)calloc(1, sizeof(task));
+        const long long lo = k * per, hi = (k + 1) * per < total ? (k + 1) * per : total;
+        if (t == NULL) {                     /* no memory for a task: run this share inline */
+            share_done(b, copy, refs, do_range(fd, write, copy, n, lo, hi));
+            continue;
+        }
+        t->b = b;
+        t->fd = fd;
+        t->write = write;
+        t->runs = copy;
+        t->n = n;
+        t->lo = lo;
+        t->hi = hi;
+        t->refs = refs;
+        pthread_mutex_lock(&q_lock);
+        if (q_tail) q_tail->next = t; else q_head = t;
+        q_tail = t;
+        pthread_cond_signal(&q_cond);
+        pthread_mutex_unlock(&q_lock);
+    }
+    return NC_NOERR;
+}
+
+int pio_wait(pio_batch *b)
+{
+    int err;
+    pthread_mutex_lock(&b->m);
+    while (b->pending > 0) pthread_cond_wait(&b->c, &b->m);
+    err = b->err;
+    b->err = NC_NOERR;
+    pthread_mutex_unlock(&b->m);
+    return err;
+}
+
+int pio_rw(int fd, int write, const pio_run *runs, size_t n)
+{
+    pio_batch b;
+    int err, e2;
+    pio_batch_init(&b);
+    err = pio_submit(&b, fd, write, runs, n);
+    e2 = pio_wait(&b);
+    pio_batch_destroy(&b);
+    return err ? err : e2;
+}

@@ -418,3 +418,47 @@ def test_numeric_data_fails_loudly_without_gpu(tmp_path):
                                                                                      N.NC_ENOTINDEFINE)
     assert N.close(ncid) == 0
     assert os.path.getsize(p) == size0
+
+
+@pytest.mark.parametrize("threads", ["1", "8"])
+def test_parallel_io_pool_large(tmp_path, threads):
+    """multi-MiB jobs split over the I/O pool (pncx_io.c): byte variables take
+    the copy path, so this runs without a GPU; checked against numpy slicing
+    of the file bytes (the pool size is fixed per process, so the env value
+    only matters for the first data call of the process)"""
+    import subprocess
+    import sys
+    code = f"""
+import os, sys, numpy as np
+sys.path.insert(0, {repr(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))})
+from pnetcdf_amd import ncfile as N, nctypes as T
+from tests import cdfparse
+p = {repr(str(tmp_path / 'big.nc'))}
+err, ncid = N.create(p, N.NC_64BIT_DATA)
+N.def_dim(ncid, 't', N.NC_UNLIMITED); N.def_dim(ncid, 'y', 1024); N.def_dim(ncid, 'x', 8192)
+N.def_var(ncid, 'b', T.NC_BYTE, [1, 2]); N.def_var(ncid, 'r', T.NC_BYTE, [0, 2])
+assert N.enddef(ncid) == 0
+a = np.random.default_rng(1).integers(-128, 127, (1024, 8192), dtype=np.int8)
+assert N.put_var(ncid, 0, a) == 0
+assert N.put_var(ncid, 0, a[100:900:4, 3:8000:5].copy(), [100, 3], [200, 1600], [4, 5]) == 0
+recs = np.random.default_rng(2).integers(-128, 127, (64, 8192), dtype=np.int8)
+reqs = [N.iput_var(ncid, 1, recs[r], [r, 0], [1, 8192])[1] for r in range(63, -1, -1)]
+assert N.wait_all(ncid, reqs)[0] == 0
+o = np.zeros((200, 1600), np.int8)
+assert N.get_var(ncid, 0, o, [100, 3], [200, 1600], [4, 5]) == 0
+assert np.array_equal(o, a[100:900:4, 3:8000:5])
+full = np.zeros((1024, 8192), np.int8)
+assert N.get_var(ncid, 0, full) == 0 and np.array_equal(full, a)
+assert N.close(ncid) == 0
+raw = np.fromfile(p, np.uint8)
+h = cdfparse.parse_cdf(raw[:4096].tobytes())
+b0 = h['vars'][0]['begin']
+assert np.array_equal(raw[b0:b0 + a.size].view(np.int8).reshape(1024, 8192), a)
+r0, rs = h['vars'][1]['begin'], h['recsize']
+for r in (0, 31, 63):
+    assert np.array_equal(raw[r0 + r * rs:r0 + r * rs + 8192].view(np.int8), recs[r])
+print('ok')
+"""
+    env = dict(os.environ, PNCX_IO_THREADS=threads)
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stderr[-2000:]
