@@ -96,6 +96,32 @@ def cpu_baseline_swap8_threads(budget_s=4.0, slab_bytes=2 << 30, threads=None):
                       f"in {el:.1f} s (orc_in_swapn, gcc -O2)"}
 
 
+def gather_leg(torch, group, buf, gib, to_cpu=False):
+    """Config 5's optional exchange, timed apart from the conversion rate
+    (SURVEY §8(e)): every rank's first `gib` GiB of converted records are
+    gathered into rank 0 (RCCL gather over xGMI).  Checksums (int64 wrapping
+    sums) of what each rank sent are compared on rank 0 with what arrived."""
+    n = min(buf.numel(), int(gib * GIB) // 8)
+    sl = buf[:n]
+    sums = group.all_gather_int(int(sl.sum().item()))
+    group.gather_slices(sl, to_cpu)                      # warm the communicator
+    torch.cuda.synchronize()
+    group.barrier()
+    t0 = time.perf_counter()
+    got = group.gather_slices(sl, to_cpu)
+    torch.cuda.synchronize()
+    group.barrier()
+    el = group.max([time.perf_counter() - t0])[0]
+    ok = True
+    if got is not None:
+        ok = all(int(g.sum().item()) == s for g, s in zip(got, sums))
+        del got
+    into = (group.world - 1) * n * 8                      # rank 0's own slice is local
+    return {"collective": "gather into rank 0 (RCCL over xGMI)" if not to_cpu else "gather into rank 0 (gloo rehearsal)",
+            "bytes_per_rank": n * 8, "bytes_into_rank0": into, "ms": round(el * 1e3, 3),
+            "GBps_into_rank0": round(into / el / 1e9, 2), "checksums_ok": ok}
+
+
 def load_traffic(kernel_key, elems_per_launch):
     """HBM traffic per launch from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, tools/pmc_summary.py; FETCH_SIZE doubled per
@@ -121,6 +147,8 @@ def main():
     ap.add_argument("--slab-gib", type=float, default=32.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--gather-gib", type=float, default=1.0,
+                    help="N>1, c2: GiB per rank gathered into rank 0 after the timed region (0 = off)")
     args = ap.parse_args()
 
     import torch
@@ -236,6 +264,11 @@ def main():
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
     elapsed, kern_ms = group.max([elapsed, kern_ms])         # max over ranks
 
+    gather = None
+    if world > 1 and args.gather_gib > 0 and args.workload == "c2":
+        gather = gather_leg(torch, group, buf, args.gather_gib,
+                            to_cpu=os.environ.get("PNCX_DIST_BACKEND", "nccl") != "nccl")
+
     moved = float(bytes_per_elem) * elems * world * args.steps
     value = moved / elapsed / GIB
     ms_per_step = elapsed * 1e3 / args.steps
@@ -269,6 +302,8 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
         }
+        if gather is not None:
+            line["gather"] = gather
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -11,6 +11,11 @@ per-rank times, and the "first error" of the conversions (NC_ERANGE is the
 only error a conversion produces, so the minimum status over ranks is the
 reference's first-error semantics, ncx.m4:2487-2488).
 
+The one data exchange is optional and reported apart from the conversion
+rate: gathering converted records into one GPU over xGMI
+(`gather_slices`, RCCL gather of device tensors) for the config-5 variant
+that hands the whole variable to a single consumer.
+
 The same helpers run over RCCL (backend "nccl", device tensors) in bench.py
 and over gloo (CPU tensors) in tests/test_shard_gloo.py.
 """
@@ -66,6 +71,27 @@ class Group:
         t = torch.tensor(list(values), dtype=torch.float64, device=self.device)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return [float(v) for v in t.cpu()]
+
+    def gather_slices(self, t, to_cpu=False):
+        """Gather one equal-size tensor per rank into rank 0 (dist.gather:
+        RCCL over xGMI for device tensors).  Returns the per-rank list on
+        rank 0 and None elsewhere."""
+        if self.dist is None:
+            return [t]
+        src = t.cpu() if to_cpu else t
+        lst = [src.new_empty(src.shape) for _ in range(self.world)] if self.rank == 0 else None
+        self.dist.gather(src, gather_list=lst, dst=0)
+        return lst
+
+    def all_gather_int(self, value):
+        """int64 value of every rank, on every rank (checksums)."""
+        if self.dist is None:
+            return [int(value)]
+        import torch
+        t = torch.tensor([int(value)], dtype=torch.int64, device=self.device)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [int(x.item()) for x in out]
 
     def first_error(self, status):
         """min over ranks of an NC status (0 = NC_NOERR, negatives = errors)."""

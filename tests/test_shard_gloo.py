@@ -89,3 +89,39 @@ def test_sharded_records_gloo(nrecs):
     assert same                      # the slabs tile the variable exactly
     assert err == st_ref == -60      # first error propagates from the rank that saw it
     assert tmax == [2.0, 2.0]        # max over ranks
+
+
+def _gather_worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = Group(dist, "cpu")
+        # each rank's converted record slab (bit patterns), as bench.py's gather leg sends it
+        mine = torch.from_numpy(np.random.default_rng(100 + rank).integers(-2**62, 2**62, 4096, dtype=np.int64))
+        sums = g.all_gather_int(int(mine.sum().item()))
+        got = g.gather_slices(mine)
+        if rank == 0:
+            ok = len(got) == world and all(int(t.sum().item()) == s for t, s in zip(got, sums))
+            exp = [np.random.default_rng(100 + r).integers(-2**62, 2**62, 4096, dtype=np.int64) for r in range(world)]
+            ok = ok and all(np.array_equal(t.numpy(), e) for t, e in zip(got, exp))
+            out_q.put(ok)
+        else:
+            assert got is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_into_rank0_gloo():
+    """config 5's optional exchange (bench.py gather leg): slabs gathered into
+    rank 0 arrive intact and match the senders' checksums"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) is True
