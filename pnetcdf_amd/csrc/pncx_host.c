@@ -362,14 +362,25 @@ static int ensure_scratch(ctx_t *c, size_t need)
  * are already pinned are used as they are; if pinning fails the pageable
  * path is used.
  */
-#define PIN_THRESHOLD (64u << 20)
+/* smallest host buffer pinned for a call (PNCX_PIN_MIN_KB, default 64 MiB) */
+size_t pncxrt_pin_threshold(void)
+{
+    static size_t v = 0;
+    if (v == 0) {
+        const char *e = getenv("PNCX_PIN_MIN_KB");
+        long kb = e ? atol(e) : 65536;
+        if (kb <= 0) kb = 65536;
+        v = (size_t)kb << 10;
+    }
+    return v;
+}
 
 typedef struct pinned_t { void *p[2]; int n; } pinned_t;
 
 static void pin_range(pinned_t *pn, const void *p, size_t bytes)
 {
     int i;
-    if (bytes < PIN_THRESHOLD || p == NULL) return;
+    if (bytes < pncxrt_pin_threshold() || p == NULL) return;
     for (i = 0; i < pn->n; i++)
         if (pn->p[i] == p) return;
     if (pncxrt_host_register((void *)p, bytes) == 0) pn->p[pn->n++] = (void *)p;

@@ -108,6 +108,8 @@ int  pncxrt_is_device_ptr(const void *p);
  * unregisters), 1 = already pinned/registered, PNCX_EDEVICE = could not */
 int  pncxrt_host_register(void *p, size_t n);
 int  pncxrt_host_unregister(void *p);
+/* host buffers at least this large are pinned for a call (pncx_host.c) */
+size_t pncxrt_pin_threshold(void);
 const char *pncxrt_last_error(void);
 
 #ifdef __cplusplus

@@ -125,3 +125,58 @@ def test_gather_into_rank0_gloo():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert q.get(timeout=10) is True
+
+
+def _file_worker(rank, world, port, path, nrecs, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pnetcdf_amd import ncfile as N
+        from pnetcdf_amd import nctypes as T
+        g = Group(dist, "cpu")
+        if rank == 0:                                   # rank 0 defines the file (the header writer)
+            err, ncid = N.create(path, N.NC_64BIT_DATA)
+            N.def_dim(ncid, "time", N.NC_UNLIMITED)
+            N.def_dim(ncid, "x", 64)
+            N.def_var(ncid, "v", T.NC_BYTE, [0, 1])
+            assert N.enddef(ncid) == 0 and N.close(ncid) == 0
+        g.barrier()
+        err, ncid = N.open(path, N.NC_WRITE)
+        assert err == 0
+        first, count = record_slab(nrecs, world, world - 1 - rank)   # rank 0 holds the LAST records
+        recs = np.stack([np.full(64, (r * 7) % 127, np.int8) for r in range(first, first + count)])
+        assert N.put_var(ncid, 0, recs, [first, 0], [count, 64]) == 0
+        mine = N.inq_dim(ncid, 0)[2]
+        numrecs = int(g.max([float(mine)])[0])          # ncmpio_sync_numrecs: MAX over ranks
+        if rank == 0:
+            assert N.sync_numrecs(ncid, numrecs) == 0
+        g.barrier()
+        assert N.close(ncid) == 0                       # rank 1 (fewer records) must not lower numrecs
+        g.barrier()
+        if rank == 0:
+            err, ncid = N.open(path)
+            ok = N.inq_dim(ncid, 0)[2] == nrecs
+            out = np.zeros((nrecs, 64), np.int8)
+            ok = ok and N.get_var(ncid, 0, out) == 0
+            ok = ok and all(np.all(out[r] == (r * 7) % 127) for r in range(nrecs))
+            N.close(ncid)
+            out_q.put(bool(ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_write_disjoint_records_gloo(tmp_path):
+    """config 5 at file level: each rank writes its record slab of one file,
+    numrecs reduced with MAX and recorded by rank 0"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    path = str(tmp_path / "shared.nc")
+    procs = [ctx.Process(target=_file_worker, args=(r, 2, port, path, 9, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) is True
