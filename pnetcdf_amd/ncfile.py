@@ -94,7 +94,9 @@ def strerror(err):
 
 
 def _b(s):
-    return s.encode() if isinstance(s, str) else s
+    # names read from a file are not validated (hdr_get_NC_name does not
+    # check them either); surrogateescape round-trips non-UTF-8 bytes
+    return s.encode("utf-8", "surrogateescape") if isinstance(s, str) else s
 
 
 def _offs(vals):
@@ -277,7 +279,7 @@ def inq_dim(ncid, dimid):
     name = ctypes.create_string_buffer(T_MAX_NAME + 1)
     n = ctypes.c_longlong()
     err = lib().pncx_nc_inq_dim(ncid, dimid, name, ctypes.byref(n))
-    return err, name.value.decode(), n.value
+    return err, name.value.decode("utf-8", "surrogateescape"), n.value
 
 
 def inq_dimid(ncid, name):
@@ -294,7 +296,7 @@ def inq_var(ncid, varid):
         return err, None, None, None, None
     dims = (ctypes.c_int * max(1, nd.value))()
     lib().pncx_nc_inq_var(ncid, varid, None, None, None, dims, None)
-    return err, name.value.decode(), xt.value, list(dims)[:nd.value], na.value
+    return err, name.value.decode("utf-8", "surrogateescape"), xt.value, list(dims)[:nd.value], na.value
 
 
 def inq_varid(ncid, name):
@@ -312,7 +314,7 @@ def inq_varoffset(ncid, varid):
 def inq_attname(ncid, varid, attnum):
     name = ctypes.create_string_buffer(T_MAX_NAME + 1)
     err = lib().pncx_nc_inq_attname(ncid, varid, attnum, name)
-    return err, name.value.decode()
+    return err, name.value.decode("utf-8", "surrogateescape")
 
 
 def inq_header_size(ncid):

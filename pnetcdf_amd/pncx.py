@@ -17,7 +17,7 @@ from . import nctypes as T
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libpncx.so")
+LIB_PATH = os.environ.get("PNCX_LIB_PATH") or os.path.join(LIB_DIR, "libpncx.so")   # override: tools/asan
 _lib = None
 
 
@@ -33,10 +33,11 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    try:
-        import torch  # noqa: F401  (share one HIP runtime with torch)
-    except ImportError:
-        pass
+    if not os.environ.get("PNCX_NO_TORCH"):          # set only by the host-only ASan run
+        try:
+            import torch  # noqa: F401  (share one HIP runtime with torch)
+        except ImportError:
+            pass
     if not os.path.exists(LIB_PATH):
         raise PncxError(T.PNCX_EDEVICE, f"{LIB_PATH} not built (run __graft_entry__.build())")
     L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
