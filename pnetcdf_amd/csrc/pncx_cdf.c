@@ -713,6 +713,9 @@ int cdf_var_shape(cdf_var *v, const cdf_hdr *h)
             v->shape[i] = h->dims[v->dimids[i]].size;
             if (v->shape[i] == 0 && i != 0) return NC_EUNLIMPOS;
         }
+        /* size check before the products, so they cannot overflow (same
+         * result as the reference, which multiplies first, ncmpio_var.c:310-332) */
+        if (!check_vlen(v, CDF_MAX_INT64 - 3)) return NC_EVARSIZE;
         if (v->ndims == 1) {
             if (v->shape[0] == 0) v->dsizes[0] = 1;
             else { v->dsizes[0] = v->shape[0]; product = v->shape[0]; }
