@@ -569,6 +569,10 @@ static int get_dims(rbuf *r, cdf_hdr *h)
         KEEP_PAD(err, status);
         if ((err = get_nn(r, &len)) != NC_NOERR) { free(name); return err; }
         if (h->unlimited_id != -1 && len == 0) { free(name); return NC_EUNLIMIT; }
+        /* NON_NEG: a CDF-5 length >= 2^63 would be negative as MPI_Offset;
+         * the reference has no check and overflows later (no fixture pins a
+         * code), so it is rejected here as a bad dimension size */
+        if (len > (unsigned long long)CDF_MAX_INT64) { free(name); return NC_EDIMSIZE; }
         err = cdf_add_dim(h, name, (long long)len);
         free(name);
         if (err) return err;
