@@ -103,6 +103,7 @@ extern "C" {
 #define NC_EINVAL_REQUEST (-212)
 #define NC_ENOENT         (-220)
 #define NC_EINTOVERFLOW   (-221)
+#define NC_ENULLSTART     (-226)
 #define NC_EINVAL_CMODE   (-228)
 #define NC_ESTRICTCDF2    (-232)
 #define NC_ENOTRECVAR     (-233)
@@ -185,6 +186,19 @@ int pncx_nc_iput_varm(int ncid, int varid, const pncx_offset *start, const pncx_
 int pncx_nc_iget_varm(int ncid, int varid, const pncx_offset *start, const pncx_offset *count,
                       const pncx_offset *stride, const pncx_offset *imap, void *buf,
                       int itype, int *reqid);
+/* varn: num subarrays (starts[i], counts[i]; counts or counts[i] NULL = one
+ * element) of one variable, packed one after another in buf
+ * (ncmpi_{put,get,iput,iget}_varn, dispatchers/var_getput.m4:426-560,
+ * ncmpio_varn.m4:38-60).  A varn request is one request id; the blocking
+ * calls are the nonblocking ones followed by a wait, as in the reference. */
+int pncx_nc_put_varn(int ncid, int varid, int num, const pncx_offset *const *starts,
+                     const pncx_offset *const *counts, const void *buf, int itype);
+int pncx_nc_get_varn(int ncid, int varid, int num, const pncx_offset *const *starts,
+                     const pncx_offset *const *counts, void *buf, int itype);
+int pncx_nc_iput_varn(int ncid, int varid, int num, const pncx_offset *const *starts,
+                      const pncx_offset *const *counts, const void *buf, int itype, int *reqid);
+int pncx_nc_iget_varn(int ncid, int varid, int num, const pncx_offset *const *starts,
+                      const pncx_offset *const *counts, void *buf, int itype, int *reqid);
 /* nreqs == NC_REQ_ALL / NC_PUT_REQ_ALL / NC_GET_REQ_ALL: every pending (put/get) request */
 int pncx_nc_wait_all(int ncid, int nreqs, int *reqids, int *statuses);
 int pncx_nc_cancel(int ncid, int nreqs, int *reqids, int *statuses);

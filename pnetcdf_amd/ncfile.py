@@ -30,7 +30,7 @@ ERR = dict(
     NC_EEDGE=-57, NC_ESTRIDE=-58, NC_EBADNAME=-59, NC_ERANGE=-60, NC_ENOMEM=-61, NC_EVARSIZE=-62,
     NC_EDIMSIZE=-63, NC_ENOTNC3=-113, NC_ENOTBUILT=-128, NC_ENULLPAD=-134, NC_EFILE=-204,
     NC_EREAD=-205, NC_EWRITE=-206, NC_ENEGATIVECNT=-210, NC_EINVAL_REQUEST=-212, NC_ENOENT=-220,
-    NC_EINTOVERFLOW=-221, NC_EINVAL_CMODE=-228, NC_ESTRICTCDF2=-232, NC_ENOTRECVAR=-233,
+    NC_EINTOVERFLOW=-221, NC_ENULLSTART=-226, NC_EINVAL_CMODE=-228, NC_ESTRICTCDF2=-232, NC_ENOTRECVAR=-233,
     NC_ENOTFILL=-234, NC_EINVAL_OMODE=-235, NC_EPENDING=-236, PNCX_EDEVICE=-1900)
 globals().update(ERR)
 ERRNAME = {v: k for k, v in ERR.items()}
@@ -80,6 +80,8 @@ def lib():
         "pncx_nc_iput_varm": [i, i, vp, vp, vp, vp, vp, i, ip],
         "pncx_nc_iget_varm": [i, i, vp, vp, vp, vp, vp, i, ip],
         "pncx_nc_wait_all": [i, i, vp, vp], "pncx_nc_cancel": [i, i, vp, vp], "pncx_nc_inq_nreqs": [i, ip],
+        "pncx_nc_put_varn": [i, i, i, vp, vp, vp, i], "pncx_nc_get_varn": [i, i, i, vp, vp, vp, i],
+        "pncx_nc_iput_varn": [i, i, i, vp, vp, vp, i, ip], "pncx_nc_iget_varn": [i, i, i, vp, vp, vp, i, ip],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -393,6 +395,54 @@ def iget_var(ncid, varid, out, start=None, count=None, stride=None, imap=None, i
     it = itype if itype is not None else itype_of(out)
     r = ctypes.c_int(NC_REQ_NULL)
     err = lib().pncx_nc_iget_varm(ncid, varid, *a, out.ctypes.data if out.size else None, it, ctypes.byref(r))
+    return err, r.value
+
+
+def _ptr_array(lists):
+    """(keep-alive, pointer) for an array of int64 vectors (starts/counts of varn);
+    None entries become NULL"""
+    if lists is None:
+        return None, None
+    arrs = [None if x is None else np.ascontiguousarray(np.asarray(x, dtype=np.int64)) for x in lists]
+    ptrs = (ctypes.c_void_p * max(1, len(arrs)))(*[None if a is None else a.ctypes.data for a in arrs])
+    return (arrs, ptrs), ctypes.cast(ptrs, ctypes.c_void_p)
+
+
+def put_varn(ncid, varid, starts, counts, buf, itype=None):
+    """ncmpi_put_varn: len(starts) subarrays packed one after another in buf"""
+    buf = np.ascontiguousarray(buf)
+    ks, ps = _ptr_array(starts)
+    kc, pc = _ptr_array(counts)
+    it = itype if itype is not None else itype_of(buf)
+    return lib().pncx_nc_put_varn(ncid, varid, len(starts) if starts is not None else 0, ps, pc,
+                                  buf.ctypes.data if buf.size else None, it)
+
+
+def get_varn(ncid, varid, starts, counts, out, itype=None):
+    ks, ps = _ptr_array(starts)
+    kc, pc = _ptr_array(counts)
+    it = itype if itype is not None else itype_of(out)
+    return lib().pncx_nc_get_varn(ncid, varid, len(starts) if starts is not None else 0, ps, pc,
+                                  out.ctypes.data if out.size else None, it)
+
+
+def iput_varn(ncid, varid, starts, counts, buf, itype=None):
+    ks, ps = _ptr_array(starts)
+    kc, pc = _ptr_array(counts)
+    it = itype if itype is not None else itype_of(buf)
+    r = ctypes.c_int(NC_REQ_NULL)
+    err = lib().pncx_nc_iput_varn(ncid, varid, len(starts), ps, pc, buf.ctypes.data if buf.size else None, it,
+                                  ctypes.byref(r))
+    return err, r.value
+
+
+def iget_varn(ncid, varid, starts, counts, out, itype=None):
+    ks, ps = _ptr_array(starts)
+    kc, pc = _ptr_array(counts)
+    it = itype if itype is not None else itype_of(out)
+    r = ctypes.c_int(NC_REQ_NULL)
+    err = lib().pncx_nc_iget_varn(ncid, varid, len(starts), ps, pc, out.ctypes.data if out.size else None, it,
+                                  ctypes.byref(r))
     return err, r.value
 
 

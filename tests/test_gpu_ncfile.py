@@ -366,3 +366,37 @@ def test_large_variable_roundtrip(gpu, tmp_path):
         h = cdfparse.parse_cdf(f.read(4096))
         f.seek(h["vars"][0]["begin"] + 8 * (n - 4))
         assert np.array_equal(np.frombuffer(f.read(32), ">f8"), a[-4:])
+
+
+def test_varn_numeric(gpu, tmp_path):
+    """put_varn / get_varn of doubles into an NC_FLOAT variable: boxes packed
+    in one buffer, one batched conversion, bytes = oracle putn per box"""
+    ora = OracleConv()
+    p = str(tmp_path / "vn.nc")
+    err, ncid = N.create(p, N.NC_64BIT_DATA)
+    N.def_dim(ncid, "y", 40)
+    N.def_dim(ncid, "x", 50)
+    N.def_var(ncid, "f", T.NC_FLOAT, [0, 1])
+    assert N.enddef(ncid) == 0
+    starts = [[0, 0], [10, 5], [39, 49], [20, 0]]
+    counts = [[3, 50], [7, 11], None, [10, 30]]
+    sizes = [150, 77, 1, 300]
+    rng = np.random.default_rng(9)
+    buf = rng.standard_normal(sum(sizes)) * 1e3
+    buf[7] = 1e300                                       # one ERANGE element
+    assert N.put_varn(ncid, 0, starts, counts, buf) == N.NC_ERANGE
+    back = np.zeros(sum(sizes), np.float64)
+    assert N.get_varn(ncid, 0, starts, counts, back) == 0
+    assert N.close(ncid) == 0
+    exp, st = ora.putn(5, T.NC_FLOAT, buf, T.ITYPE_DOUBLE, T.fill_bytes(T.NC_FLOAT))
+    assert st == N.NC_ERANGE
+    e_back, _ = ora.getn(5, T.NC_FLOAT, exp, T.ITYPE_DOUBLE)
+    assert back.tobytes() == e_back.tobytes()
+    raw = _raw(p)
+    h = cdfparse.parse_cdf(raw)
+    f = np.frombuffer(_var_bytes(raw, h, "f", None, 40 * 50 * 4), ">f4").reshape(40, 50)
+    e = np.frombuffer(exp, ">f4")
+    assert f[0:3, :].tobytes() == e[:150].tobytes()
+    assert f[10:17, 5:16].tobytes() == e[150:227].tobytes()
+    assert f[39, 49].tobytes() == e[227:228].tobytes()
+    assert f[20:30, 0:30].tobytes() == e[228:].tobytes()

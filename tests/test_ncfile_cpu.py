@@ -462,3 +462,37 @@ print('ok')
     env = dict(os.environ, PNCX_IO_THREADS=threads)
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stderr[-2000:]
+
+
+def test_varn_text_and_byte(tmp_path):
+    """ncmpi_put_varn / get_varn / iput_varn (dispatchers/var_getput.m4:426-560):
+    several boxes packed in one buffer; var1 boxes (counts[i] None); errors"""
+    p = str(tmp_path / "vn.nc")
+    ncid = _text_file(p)
+    starts = [[0, 0], [4, 1], [9, 5], [1, 3]]          # disjoint boxes (overlap order is undefined)
+    counts = [[1, 6], [2, 3], None, [3, 2]]
+    buf = _chars("ABCDEF" + "ghijkl" + "Z" + "mnopqr")
+    assert N.put_varn(ncid, 0, starts, counts, buf) == 0
+    exp = np.full((10, 6), b"\x00", "S1")
+    exp[0, 0:6] = list(b"ABCDEF"[i:i + 1] for i in range(6))
+    exp[4:6, 1:4] = np.frombuffer(b"ghijkl", "S1").reshape(2, 3)
+    exp[9, 5] = b"Z"
+    exp[1:4, 3:5] = np.frombuffer(b"mnopqr", "S1").reshape(3, 2)
+    out = np.zeros(60, "S1")
+    assert N.get_var(ncid, 0, out) == 0 and out.tobytes() == exp.tobytes()
+    back = np.zeros(19, "S1")
+    assert N.get_varn(ncid, 0, starts, counts, back) == 0 and back.tobytes() == buf.tobytes()
+    # nonblocking varn on a record variable: one request id, numrecs grows
+    err, rq = N.iput_varn(ncid, 3, [[6], [1], [3]], [[2], [1], [1]], np.array([1, 2, 3, 4], np.int8))
+    assert err == 0 and rq >= 0
+    err, rq2 = N.iput_var(ncid, 3, np.array([9], np.int8), [0], [1])
+    assert N.wait_all(ncid, [rq, rq2]) == (0, [0, 0])
+    assert N.inq_dim(ncid, 0)[2] == 8
+    o = np.zeros(8, np.int8)
+    assert N.get_var(ncid, 3, o, [0], [8]) == 0 and o.tolist() == [9, 3, 0, 4, 0, 0, 1, 2]
+    # errors: NULL starts, bad box (nothing posted), zero boxes
+    assert N.put_varn(ncid, 0, None, None, buf) == 0                      # num 0: nothing to do
+    assert N.lib().pncx_nc_put_varn(ncid, 0, 2, None, None, buf.ctypes.data, T.ITYPE_CHAR) == N.NC_ENULLSTART
+    assert N.put_varn(ncid, 0, [[0, 0], [11, 0]], [[1, 2], [1, 2]], buf[:4].copy()) == N.NC_EINVALCOORDS
+    assert N.inq_nreqs(ncid) == (0, 0)
+    assert N.close(ncid) == 0
