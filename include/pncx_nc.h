@@ -101,6 +101,10 @@ extern "C" {
 #define NC_EWRITE         (-206)
 #define NC_ENEGATIVECNT   (-210)
 #define NC_EINVAL_REQUEST (-212)
+#define NC_EPREVATTACHBUF (-216)
+#define NC_ENULLABUF      (-217)
+#define NC_EPENDINGBPUT   (-218)
+#define NC_EINSUFFBUF     (-219)
 #define NC_ENOENT         (-220)
 #define NC_EINTOVERFLOW   (-221)
 #define NC_ENULLSTART     (-226)
@@ -199,6 +203,18 @@ int pncx_nc_iput_varn(int ncid, int varid, int num, const pncx_offset *const *st
                       const pncx_offset *const *counts, const void *buf, int itype, int *reqid);
 int pncx_nc_iget_varn(int ncid, int varid, int num, const pncx_offset *const *starts,
                       const pncx_offset *const *counts, void *buf, int itype, int *reqid);
+/* buffered puts (ncmpi_buffer_attach / bput_var* / buffer_detach,
+ * ncmpio_bput.c, ncmpio_i_getput.m4:266-310): the data are converted into the
+ * attached buffer when posted, so the caller may reuse its buffer at once;
+ * wait_all only writes.  Space is the external size of each request; it is
+ * released at wait (tail first, as abuf_coalesce, ncmpio_wait.c:37-56). */
+int pncx_nc_buffer_attach(int ncid, pncx_offset bufsize);
+int pncx_nc_buffer_detach(int ncid);
+int pncx_nc_inq_buffer_size(int ncid, pncx_offset *size);
+int pncx_nc_inq_buffer_usage(int ncid, pncx_offset *usage);
+int pncx_nc_bput_varm(int ncid, int varid, const pncx_offset *start, const pncx_offset *count,
+                      const pncx_offset *stride, const pncx_offset *imap, const void *buf,
+                      int itype, int *reqid);
 /* nreqs == NC_REQ_ALL / NC_PUT_REQ_ALL / NC_GET_REQ_ALL: every pending (put/get) request */
 int pncx_nc_wait_all(int ncid, int nreqs, int *reqids, int *statuses);
 int pncx_nc_cancel(int ncid, int nreqs, int *reqids, int *statuses);

@@ -29,7 +29,8 @@ ERR = dict(
     NC_ENOTVAR=-49, NC_EGLOBAL=-50, NC_ENOTNC=-51, NC_EMAXNAME=-53, NC_EUNLIMIT=-54, NC_ECHAR=-56,
     NC_EEDGE=-57, NC_ESTRIDE=-58, NC_EBADNAME=-59, NC_ERANGE=-60, NC_ENOMEM=-61, NC_EVARSIZE=-62,
     NC_EDIMSIZE=-63, NC_ENOTNC3=-113, NC_ENOTBUILT=-128, NC_ENULLPAD=-134, NC_EFILE=-204,
-    NC_EREAD=-205, NC_EWRITE=-206, NC_ENEGATIVECNT=-210, NC_EINVAL_REQUEST=-212, NC_ENOENT=-220,
+    NC_EREAD=-205, NC_EWRITE=-206, NC_ENEGATIVECNT=-210, NC_EINVAL_REQUEST=-212, NC_EPREVATTACHBUF=-216,
+    NC_ENULLABUF=-217, NC_EPENDINGBPUT=-218, NC_EINSUFFBUF=-219, NC_ENOENT=-220,
     NC_EINTOVERFLOW=-221, NC_ENULLSTART=-226, NC_EINVAL_CMODE=-228, NC_ESTRICTCDF2=-232, NC_ENOTRECVAR=-233,
     NC_ENOTFILL=-234, NC_EINVAL_OMODE=-235, NC_EPENDING=-236, PNCX_EDEVICE=-1900)
 globals().update(ERR)
@@ -80,6 +81,9 @@ def lib():
         "pncx_nc_iput_varm": [i, i, vp, vp, vp, vp, vp, i, ip],
         "pncx_nc_iget_varm": [i, i, vp, vp, vp, vp, vp, i, ip],
         "pncx_nc_wait_all": [i, i, vp, vp], "pncx_nc_cancel": [i, i, vp, vp], "pncx_nc_inq_nreqs": [i, ip],
+        "pncx_nc_buffer_attach": [i, ll], "pncx_nc_buffer_detach": [i],
+        "pncx_nc_inq_buffer_size": [i, lp], "pncx_nc_inq_buffer_usage": [i, lp],
+        "pncx_nc_bput_varm": [i, i, vp, vp, vp, vp, vp, i, ip],
         "pncx_nc_put_varn": [i, i, i, vp, vp, vp, i], "pncx_nc_get_varn": [i, i, i, vp, vp, vp, i],
         "pncx_nc_iput_varn": [i, i, i, vp, vp, vp, i, ip], "pncx_nc_iget_varn": [i, i, i, vp, vp, vp, i, ip],
     }
@@ -443,6 +447,34 @@ def iget_varn(ncid, varid, starts, counts, out, itype=None):
     r = ctypes.c_int(NC_REQ_NULL)
     err = lib().pncx_nc_iget_varn(ncid, varid, len(starts), ps, pc, out.ctypes.data if out.size else None, it,
                                   ctypes.byref(r))
+    return err, r.value
+
+
+def buffer_attach(ncid, size):
+    return lib().pncx_nc_buffer_attach(ncid, size)
+
+
+def buffer_detach(ncid):
+    return lib().pncx_nc_buffer_detach(ncid)
+
+
+def inq_buffer_size(ncid):
+    o = ctypes.c_longlong()
+    return lib().pncx_nc_inq_buffer_size(ncid, ctypes.byref(o)), o.value
+
+
+def inq_buffer_usage(ncid):
+    o = ctypes.c_longlong()
+    return lib().pncx_nc_inq_buffer_usage(ncid, ctypes.byref(o)), o.value
+
+
+def bput_var(ncid, varid, buf, start=None, count=None, stride=None, imap=None, itype=None):
+    """ncmpi_bput_var*: converted into the attached buffer now; buf is free on return"""
+    buf = np.ascontiguousarray(buf)
+    keep, a = _args(start, count, stride, imap)
+    it = itype if itype is not None else itype_of(buf)
+    r = ctypes.c_int(NC_REQ_NULL)
+    err = lib().pncx_nc_bput_varm(ncid, varid, *a, buf.ctypes.data if buf.size else None, it, ctypes.byref(r))
     return err, r.value
 
 

@@ -400,3 +400,28 @@ def test_varn_numeric(gpu, tmp_path):
     assert f[10:17, 5:16].tobytes() == e[150:227].tobytes()
     assert f[39, 49].tobytes() == e[227:228].tobytes()
     assert f[20:30, 0:30].tobytes() == e[228:].tobytes()
+
+
+def test_bput_numeric(gpu, tmp_path):
+    """buffered puts of doubles into NC_SHORT: converted at post (NC_ERANGE
+    reported there), written at wait"""
+    ora = OracleConv()
+    p = str(tmp_path / "bp.nc")
+    err, ncid = N.create(p, N.NC_64BIT_DATA)
+    N.def_dim(ncid, "x", 1000)
+    N.def_var(ncid, "s", T.NC_SHORT, [0])
+    assert N.enddef(ncid) == 0
+    assert N.buffer_attach(ncid, 2000) == 0
+    d = np.linspace(-50000, 50000, 1000)
+    err, r1 = N.bput_var(ncid, 0, d[:500].copy(), [0], [500])
+    assert err == N.NC_ERANGE and r1 >= 0
+    err, r2 = N.bput_var(ncid, 0, d[500:].copy(), [500], [500])
+    assert err == N.NC_ERANGE
+    assert N.inq_buffer_usage(ncid) == (0, 2000)
+    assert N.wait_all(ncid, [r1, r2]) == (0, [0, 0])
+    assert N.buffer_detach(ncid) == 0
+    assert N.close(ncid) == 0
+    exp, _ = ora.putn(5, T.NC_SHORT, d, T.ITYPE_DOUBLE, T.fill_bytes(T.NC_SHORT))
+    raw = _raw(p)
+    h = cdfparse.parse_cdf(raw)
+    assert _var_bytes(raw, h, "s", None, 2000) == exp

@@ -496,3 +496,34 @@ def test_varn_text_and_byte(tmp_path):
     assert N.put_varn(ncid, 0, [[0, 0], [11, 0]], [[1, 2], [1, 2]], buf[:4].copy()) == N.NC_EINVALCOORDS
     assert N.inq_nreqs(ncid) == (0, 0)
     assert N.close(ncid) == 0
+
+
+def test_bput_attached_buffer(tmp_path):
+    """ncmpio_bput.c / ncmpio_i_getput.m4:266-310: bput converts into the
+    attached buffer at post time (the caller's buffer may change right
+    after), usage accounting, NC_EINSUFFBUF / NC_ENULLABUF /
+    NC_EPREVATTACHBUF / NC_EPENDINGBPUT, tail-first release at wait"""
+    p = str(tmp_path / "bp.nc")
+    ncid = _text_file(p)
+    row = _chars("abcdef")
+    assert N.bput_var(ncid, 0, row, [0, 0], [1, 6])[0] == N.NC_ENULLABUF
+    assert N.buffer_attach(ncid, 20) == 0
+    assert N.buffer_attach(ncid, 20) == N.NC_EPREVATTACHBUF
+    assert N.inq_buffer_size(ncid) == (0, 20)
+    err, r1 = N.bput_var(ncid, 0, row, [0, 0], [1, 6])
+    assert err == 0
+    row[:] = _chars("XXXXXX")                          # caller reuses its buffer immediately
+    err, r2 = N.bput_var(ncid, 0, _chars("ghijkl"), [1, 0], [1, 6])
+    assert N.inq_buffer_usage(ncid) == (0, 12)
+    assert N.bput_var(ncid, 0, _chars("mnopqrstu"), [2, 0], [1, 9])[0] == N.NC_EEDGE
+    assert N.bput_var(ncid, 0, np.zeros(12, "S1"), [2, 0], [2, 6])[0] == N.NC_EINSUFFBUF
+    assert N.buffer_detach(ncid) == N.NC_EPENDINGBPUT
+    assert N.wait_all(ncid, [r2]) == (0, [0])          # r2 is at the tail: its space comes back
+    assert N.inq_buffer_usage(ncid) == (0, 6)
+    assert N.wait_all(ncid, [r1]) == (0, [0])
+    assert N.inq_buffer_usage(ncid) == (0, 0)
+    assert N.buffer_detach(ncid) == 0
+    assert N.buffer_detach(ncid) == N.NC_ENULLABUF
+    o = np.zeros(12, "S1")
+    assert N.get_var(ncid, 0, o, [0, 0], [2, 6]) == 0 and o.tobytes() == b"abcdefghijkl"
+    assert N.close(ncid) == 0

@@ -74,6 +74,15 @@ def data_paths(td):
     N.wait_all(ncid)
     for bad in ([40, 0], [-1, 0], [0, 999]):
         N.put_var(ncid, 0, a[:10].copy(), bad, [1, 10])
+    # varn and buffered puts (copy paths)
+    N.put_varn(ncid, 0, [[0, 0], [5, 5], [7, 0]], [[1, 10], None, [2, 3]], a[:17].copy())
+    o17 = np.zeros(17, "S1")
+    N.get_varn(ncid, 0, [[0, 0], [5, 5], [7, 0]], [[1, 10], None, [2, 3]], o17)
+    N.buffer_attach(ncid, 4096)
+    rq = [N.bput_var(ncid, 1, b[:100].copy(), [k, 0], [1, 100])[1] for k in range(5)]
+    N.bput_var(ncid, 1, b[:4000].copy(), [0, 0], [4, 1000])           # NC_EINSUFFBUF
+    N.wait_all(ncid, rq[::-1])
+    N.buffer_detach(ncid)
     assert N.redef(ncid) == 0
     for k in range(30):
         N.put_att_text(ncid, N.NC_GLOBAL, f"a{k}", "x" * k)
