@@ -428,13 +428,15 @@ long long cdf_hdr_encode(const cdf_hdr *h, unsigned char *buf)
 /* ------------------------------------------------------------------------ */
 typedef struct rbuf {
     const unsigned char *b;
-    size_t len, pos, limit;     /* bytes past len read as zero, up to limit */
+    size_t len, pos, limit;     /* bytes past the file end read as zero, up to limit */
+    size_t file_size;
     int nn, format, strict;
 } rbuf;
 
 static int get_bytes(rbuf *r, void *out, size_t n)
 {
     size_t have;
+    if (r->pos + n > r->len && r->len < r->file_size) return CDF_NEED_MORE;  /* not read yet */
     if (r->pos + n > r->limit) return NC_ENOTNC;    /* header runs past the file */
     have = r->pos < r->len ? r->len - r->pos : 0;
     if (have > n) have = n;
@@ -654,16 +656,18 @@ static int compute_var_shape(cdf_hdr *h)
     return NC_NOERR;
 }
 
-int cdf_hdr_decode(const unsigned char *buf, size_t len, cdf_hdr *h, int strict_pad)
+int cdf_hdr_decode(const unsigned char *buf, size_t len, size_t file_size, cdf_hdr *h, int strict_pad)
 {
     rbuf r;
     int err, status = NC_NOERR, i;
     unsigned long long nrec;
     cdf_hdr_init(h, 0);
+    if (len > file_size) len = file_size;
     r.b = buf;
     r.len = len;
+    r.file_size = file_size;
     r.pos = 0;
-    r.limit = len + CDF_HDR_CHUNK;
+    r.limit = file_size + CDF_HDR_CHUNK;
     r.strict = strict_pad;
     if (len < 4 || memcmp(buf, "CDF", 3) != 0) return NC_ENOTNC;
     if (buf[3] != 1 && buf[3] != 2 && buf[3] != 5) return NC_ENOTNC;

@@ -81,12 +81,16 @@ long long cdf_hdr_len(const cdf_hdr *h);
 /* Encode into buf (at least cdf_hdr_len bytes).  Returns bytes written or a
  * negative NC error. */
 long long cdf_hdr_encode(const cdf_hdr *h, unsigned char *buf);
-/* Decode from buf[0..len) (bytes past the end read as zero, as the
- * reference's chunked fetch does, up to one chunk).  strict_pad: report
- * non-null header padding as NC_ENULLPAD (ncvalidator behaviour).  On
- * success the layout fields are recomputed (compute_var_shape) and the
- * header is validated (check_vlens, check_voffs). */
-int       cdf_hdr_decode(const unsigned char *buf, size_t len, cdf_hdr *h, int strict_pad);
+/* Decode from buf[0..len), the first len bytes of a file of file_size
+ * bytes.  Bytes past the end of the FILE read as zero (the reference's
+ * chunked fetch zero-fills a short read), up to one chunk; when the decoder
+ * needs bytes in [len, file_size) it returns CDF_NEED_MORE and the caller
+ * reads more and retries.  strict_pad: report non-null header padding as
+ * NC_ENULLPAD (ncvalidator).  On success the layout fields are recomputed
+ * (compute_var_shape) and the header is validated (check_vlens,
+ * check_voffs). */
+#define CDF_NEED_MORE 1
+int       cdf_hdr_decode(const unsigned char *buf, size_t len, size_t file_size, cdf_hdr *h, int strict_pad);
 
 int       cdf_check_name(const char *name);
 int       cdf_find_dim(const cdf_hdr *h, const char *name);

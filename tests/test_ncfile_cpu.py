@@ -527,3 +527,26 @@ def test_bput_attached_buffer(tmp_path):
     o = np.zeros(12, "S1")
     assert N.get_var(ncid, 0, o, [0, 0], [2, 6]) == 0 and o.tobytes() == b"abcdefghijkl"
     assert N.close(ncid) == 0
+
+
+def test_header_larger_than_read_chunk(tmp_path):
+    """a header past the 256 KiB first read (nc_header_read_chunk_size):
+    open reads more instead of decoding zeros"""
+    p = str(tmp_path / "bighdr.nc")
+    err, ncid = N.create(p, N.NC_64BIT_DATA)
+    N.def_dim(ncid, "x", 16)
+    N.def_var(ncid, "b", T.NC_BYTE, [0])
+    for k in range(2500):
+        assert N.put_att_text(ncid, N.NC_GLOBAL, f"attribute_{k:05d}", f"{k:05d}" * 20) == 0
+    assert N.enddef(ncid) == 0
+    assert N.inq_header_size(ncid)[1] > 300000
+    assert N.put_var(ncid, 0, np.arange(16, dtype=np.int8)) == 0
+    assert N.close(ncid) == 0
+    err, ncid = N.open(p)
+    assert err == 0
+    assert N.inq(ncid)[3] == 2500
+    assert N.get_att(ncid, N.NC_GLOBAL, "attribute_02499") == (0, b"02499" * 20)
+    o = np.zeros(16, np.int8)
+    assert N.get_var(ncid, 0, o) == 0 and o.tolist() == list(range(16))
+    assert N.close(ncid) == 0
+    assert N.validate(p) == 0
