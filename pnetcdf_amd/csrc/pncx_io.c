@@ -6,11 +6,24 @@
  * one thread does at a few GB/s.  Splitting the copy over the host cores the
  * box gives a GPU (PNCX_IO_THREADS, default 8) raises that, and running it
  * asynchronously lets it overlap the GPU conversion of the next chunk.
+ *
+ * Writes: pwrite into one file serialises on the inode lock, so more threads
+ * do not help (measured on tmpfs: 4.8 GB/s with 1 thread, 4.3 with 8).
+ * Copies into a shared mapping of the file do scale (49 GB/s with 8
+ * threads, 4 GB/s on first touch vs 2 for pwrite).  Large write runs
+ * therefore go through mmap + memcpy: the pool first grows the file with
+ * fallocate (never shrinks it, so ranks writing disjoint records of one file
+ * stay safe), then each task maps its page-aligned window.  Runs under
+ * MMAP_MIN bytes, file systems without fallocate and PNCX_IO_MMAP=0 use
+ * pwrite.  Reads use pread, which takes the shared lock and scales.
  */
 #define _GNU_SOURCE
 #include <errno.h>
+#include <fcntl.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include "pncx.h"
@@ -20,11 +33,12 @@
 #define MAX_THREADS 64
 #define INLINE_BYTES (1u << 20)      /* below this a job runs in the caller */
 #define MIN_TASK_BYTES (1u << 20)    /* no task smaller than this */
+#define MMAP_MIN (256u << 10)        /* smallest write run copied through a mapping */
 
 typedef struct task {
     struct task *next;
     pio_batch *b;
-    int fd, write;
+    int fd, write;                   /* write: 1 = pwrite, 2 = mmap + memcpy for large runs */
     pio_run *runs;                   /* shared by the tasks of one job */
     size_t n;
     long long lo, hi;                /* byte range of the concatenated runs */
@@ -63,6 +77,20 @@ int pio_read_all(int fd, void *buf, size_t n, long long off)
     return NC_NOERR;
 }
 
+static long g_page;
+
+/* memcpy into a shared mapping of the file (the range lies inside the file) */
+static int map_write(int fd, const unsigned char *src, size_t n, long long off)
+{
+    const long long base = off - off % g_page;
+    const size_t span = (size_t)(off - base) + n;
+    unsigned char *m = (unsigned char *)mmap(NULL, span, PROT_WRITE, MAP_SHARED, fd, (off_t)base);
+    if (m == MAP_FAILED) return pio_write_all(fd, src, n, off);
+    memcpy(m + (off - base), src, n);
+    munmap(m, span);
+    return NC_NOERR;
+}
+
 /* copy bytes [lo, hi) of the concatenation of runs */
 static int do_range(int fd, int write, const pio_run *runs, size_t n, long long lo, long long hi)
 {
@@ -76,11 +104,45 @@ static int do_range(int fd, int write, const pio_run *runs, size_t n, long long 
         {
             const long long s = a > lo ? a : lo, e = b < hi ? b : hi;
             const long long k = s - a;
-            err = write ? pio_write_all(fd, runs[i].mem + k, (size_t)(e - s), runs[i].off + k)
-                        : pio_read_all(fd, runs[i].mem + k, (size_t)(e - s), runs[i].off + k);
+            if (!write)
+                err = pio_read_all(fd, runs[i].mem + k, (size_t)(e - s), runs[i].off + k);
+            else if (write == 2 && e - s >= (long long)MMAP_MIN)
+                err = map_write(fd, runs[i].mem + k, (size_t)(e - s), runs[i].off + k);
+            else
+                err = pio_write_all(fd, runs[i].mem + k, (size_t)(e - s), runs[i].off + k);
         }
     }
     return err;
+}
+
+static int mmap_mode(void)
+{
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("PNCX_IO_MMAP");
+        v = e ? atoi(e) != 0 : 1;
+        g_page = sysconf(_SC_PAGESIZE);
+        if (g_page <= 0) g_page = 4096;
+    }
+    return v;
+}
+
+/* Write job through mappings?  The file must already cover every large run:
+ * grow it with fallocate where needed (a mapping cannot extend a file). */
+static int write_mode(int fd, const pio_run *runs, size_t n, long long total)
+{
+    struct stat st;
+    long long end = 0;
+    size_t i;
+    if (!mmap_mode() || total < (long long)MMAP_MIN) return 1;
+    for (i = 0; i < n; i++)
+        if (runs[i].len >= (long long)MMAP_MIN && runs[i].off + runs[i].len > end) end = runs[i].off + runs[i].len;
+    if (end == 0) return 1;
+    if (fstat(fd, &st) != 0) return 1;
+    if (end > (long long)st.st_size &&
+        fallocate(fd, 0, (off_t)st.st_size, (off_t)(end - (long long)st.st_size)) != 0)
+        return 1;
+    return 2;
 }
 
 /* one share of a job is done: record its error, release the shared runs */
@@ -164,6 +226,7 @@ int pio_submit(pio_batch *b, int fd, int write, const pio_run *runs, size_t n)
     pio_run *copy;
     for (i = 0; i < n; i++) total += runs[i].len;
     if (total == 0) return NC_NOERR;
+    if (write) write = write_mode(fd, runs, n, total);
     nt = total < INLINE_BYTES ? 0 : pio_threads();
     if (nt <= 1) {
         const int err = do_range(fd, write, runs, n, 0, total);

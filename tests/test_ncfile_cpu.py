@@ -420,8 +420,8 @@ def test_numeric_data_fails_loudly_without_gpu(tmp_path):
     assert os.path.getsize(p) == size0
 
 
-@pytest.mark.parametrize("threads", ["1", "8"])
-def test_parallel_io_pool_large(tmp_path, threads):
+@pytest.mark.parametrize("threads,mmap", [("1", "0"), ("8", "0"), ("8", "1")])
+def test_parallel_io_pool_large(tmp_path, threads, mmap):
     """multi-MiB jobs split over the I/O pool (pncx_io.c): byte variables take
     the copy path, so this runs without a GPU; checked against numpy slicing
     of the file bytes (the pool size is fixed per process, so the env value
@@ -459,7 +459,7 @@ for r in (0, 31, 63):
     assert np.array_equal(raw[r0 + r * rs:r0 + r * rs + 8192].view(np.int8), recs[r])
 print('ok')
 """
-    env = dict(os.environ, PNCX_IO_THREADS=threads)
+    env = dict(os.environ, PNCX_IO_THREADS=threads, PNCX_IO_MMAP=mmap)
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stderr[-2000:]
 
