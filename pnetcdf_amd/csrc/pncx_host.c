@@ -362,14 +362,15 @@ static int ensure_scratch(ctx_t *c, size_t need)
  * are already pinned are used as they are; if pinning fails the pageable
  * path is used.
  */
-/* smallest host buffer pinned for a call (PNCX_PIN_MIN_KB, default 64 MiB) */
+/* smallest host buffer pinned for a call (PNCX_PIN_MIN_KB, default 1 MiB:
+ * the file-level sweep of 256 KiB / 1 MiB / 64 MiB, profiles/r01_file_bench_pin*.json) */
 size_t pncxrt_pin_threshold(void)
 {
     static size_t v = 0;
     if (v == 0) {
         const char *e = getenv("PNCX_PIN_MIN_KB");
-        long kb = e ? atol(e) : 65536;
-        if (kb <= 0) kb = 65536;
+        long kb = e ? atol(e) : 1024;
+        if (kb <= 0) kb = 1024;
         v = (size_t)kb << 10;
     }
     return v;
