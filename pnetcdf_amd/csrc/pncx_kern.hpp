@@ -148,15 +148,37 @@ __device__ __forceinline__ void vec_step(const uint8_t *src, uint8_t *dst,
     for (int k = 0; k < ND; k++) st16<NT>(dst + 16 * k, ov[k]);
 }
 
-__device__ __forceinline__ void publish_status(int *status, bool bad) {
+// value: NC_ERANGE, or for batches the per-call epoch value (pncx_dev_batch
+// then needs no zeroing of the status words between calls)
+__device__ __forceinline__ void publish_status(int *status, bool bad, int value = NC_ERANGE) {
     if (status == nullptr) return;
     const unsigned long long m = __ballot(bad);
     // Every out-of-range wave would otherwise store into the same word: with
     // mostly-ERANGE data that serialises millions of atomics (measured 40 GB/s).
     // Read first (relaxed, agent scope: L2) and store only if not yet set.
     if (m != 0 && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)m) - 1) &&
-        __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != NC_ERANGE)
-        __hip_atomic_store(status, NC_ERANGE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != value)
+        __hip_atomic_store(status, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// block -> segment of a batch grid: equal-size segments divide directly, a
+// few runs of equal sizes (e.g. NC_SHORT and NC_FLOAT variables) scan the
+// group table passed by value, anything else reads the device map
+__device__ __forceinline__ int batch_segment(long long b, long long uniform, const int *map,
+                                             const pncxk_groups &g, const pncxk_seg *segs, int nseg) {
+    if (uniform > 0) return (int)(b / uniform);
+    if (g.n > 0) {
+        int k = 0;
+        while (k + 1 < g.n && b >= g.b0[k + 1]) k++;
+        return g.s0[k] + (int)((b - g.b0[k]) / g.per[k]);
+    }
+    if (map != nullptr) return map[b];
+    int lo = 0, hi = nseg - 1;             // binary search (sorted by block0)
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (segs[mid].block0 <= b) lo = mid; else hi = mid - 1;
+    }
+    return lo;
 }
 
 // XCD-contiguous block order: under the observed round-robin dispatch,
@@ -358,23 +380,11 @@ constexpr int BATCH_STEPS = 1;  // tiles per block
 
 template <class Op, bool NT>
 __global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg, long long uniform,
-                                               const int *map) {
+                                               const int *map, pncxk_groups grp, int sval) {
     using S = Shape<Op>;
     __shared__ __attribute__((aligned(16))) uint8_t lds[S::USE_LDS ? 4096 : 16];
     const long long b = blockIdx.x;
-    int lo;
-    if (uniform > 0) {                     // equal-size segments: direct
-        lo = (int)(b / uniform);
-    } else if (map != nullptr) {           // block -> segment table
-        lo = map[b];
-    } else {                               // binary search (sorted by block0)
-        int hi = nseg - 1;
-        lo = 0;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (segs[mid].block0 <= b) lo = mid; else hi = mid - 1;
-        }
-    }
+    const int lo = batch_segment(b, uniform, map, grp, segs, nseg);
     const pncxk_seg sg = segs[lo];
     const uint8_t *src = (const uint8_t *)sg.src;
     uint8_t *dst = (uint8_t *)sg.dst;
@@ -389,7 +399,7 @@ __global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg, 
     if (rel < ntile)
         tile_body<Op, NT>(src + (sg.head + rel * (int64_t)S::TILE) * S::SS,
                           dst + (sg.head + rel * (int64_t)S::TILE) * S::DS, fill, bad, lds);
-    publish_status(sg.status, bad);
+    publish_status(sg.status, bad, sval);
 }
 
 // ---------------------------------------------------------------------------
@@ -504,7 +514,7 @@ int launch_batch(const pncxk_batch_args *a) {
     if (a->nblocks <= 0) return 0;
     if constexpr (Op::PRESERVE) return NC_EINVAL;   // host runs these one by one
     hipLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0,
-                       (hipStream_t)a->stream, a->dsegs, a->nseg, a->uniform, a->dmap);
+                       (hipStream_t)a->stream, a->dsegs, a->nseg, a->uniform, a->dmap, a->grp, a->sval);
     return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
 }
 

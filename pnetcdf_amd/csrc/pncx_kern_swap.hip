@@ -136,10 +136,10 @@ extern "C" int pncxk_opinfo_getput(int kind, int xtype, int itype, int preserve,
 // is the same as for the single-size classes.
 template <bool NT>
 __global__ __launch_bounds__(256) void k_batch_swapmix(const pncxk_seg *segs, int nseg, long long uniform,
-                                                       const int *map) {
+                                                       const int *map, pncxk_groups grp, int sval) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[16];
     const long long b = blockIdx.x;
-    const int s = uniform > 0 ? (int)(b / uniform) : map[b];
+    const int s = batch_segment(b, uniform, map, grp, segs, nseg);
     const pncxk_seg sg = segs[s];
     const uint8_t *src = (const uint8_t *)sg.src;
     uint8_t *dst = (uint8_t *)sg.dst;
@@ -163,14 +163,15 @@ __global__ __launch_bounds__(256) void k_batch_swapmix(const pncxk_seg *segs, in
 #undef PNCX_MIX
         default: break;
     }
-    (void)nseg;
+    (void)sval;    // swaps never produce NC_ERANGE
 }
 
 extern "C" int pncxk_batch(int kind, int a, int b, int c, const pncxk_batch_args *args) {
     if (kind == PNCXK_SWAPMIX) {
         if (args->nblocks <= 0) return 0;
         hipLaunchKernelGGL((k_batch_swapmix<true>), dim3((unsigned)args->nblocks), dim3(256), 0,
-                           (hipStream_t)args->stream, args->dsegs, args->nseg, args->uniform, args->dmap);
+                           (hipStream_t)args->stream, args->dsegs, args->nseg, args->uniform, args->dmap,
+                           args->grp, args->sval);
         return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
     }
     if (kind == PNCXK_SWAP) {
@@ -295,6 +296,12 @@ int pncxrt_stream_wait_event(void *s, void *e) {
 int pncxrt_event_sync(void *e) { return rt(hipEventSynchronize((hipEvent_t)e), "hipEventSynchronize"); }
 int pncxrt_event_elapsed_ms(float *ms, void *a, void *b) {
     return rt(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b), "hipEventElapsedTime");
+}
+int pncxrt_event_query(void *e) {
+    const hipError_t r = hipEventQuery((hipEvent_t)e);
+    if (r == hipSuccess) return 1;
+    if (r == hipErrorNotReady) { (void)hipGetLastError(); return 0; }
+    return rt(r, "hipEventQuery");
 }
 int pncxrt_host_register(void *p, size_t n) {
     /* hipHostRegister on an already registered range returns success and a

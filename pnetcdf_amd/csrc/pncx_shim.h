@@ -36,12 +36,24 @@ typedef struct pncxk_seg {
     int                aux;    /* SWAPMIX: element size of this segment       */
 } pncxk_seg;
 
+/* up to PNCXK_MAXGRP runs of equal-size segments: block b of the grid is in
+ * group g when b0[g] <= b < b0[g+1], segment s0[g] + (b - b0[g]) / per[g] */
+#define PNCXK_MAXGRP 8
+typedef struct pncxk_groups {
+    int       n;
+    int       s0[PNCXK_MAXGRP];
+    long long b0[PNCXK_MAXGRP];
+    long long per[PNCXK_MAXGRP];
+} pncxk_groups;
+
 typedef struct pncxk_batch_args {
     const pncxk_seg *dsegs;    /* device array, sorted by block0           */
     int              nseg;
     long long        nblocks;
     long long        uniform;  /* blocks per segment if all equal, else 0  */
     int             *dmap;     /* device block->segment table or NULL      */
+    pncxk_groups     grp;      /* used when uniform == 0 and grp.n > 0     */
+    int              sval;     /* value a segment's status word gets on ERANGE */
     void            *stream;
 } pncxk_batch_args;
 
@@ -102,6 +114,8 @@ int  pncxrt_event_destroy(void *e);
 int  pncxrt_event_record(void *e, void *stream);
 int  pncxrt_stream_wait_event(void *stream, void *e);
 int  pncxrt_event_sync(void *e);
+/* 1 = done, 0 = not yet, PNCX_EDEVICE = error */
+int  pncxrt_event_query(void *e);
 int  pncxrt_event_elapsed_ms(float *ms, void *start, void *stop);
 int  pncxrt_is_device_ptr(const void *p);
 /* pin a pageable host range for DMA: 0 = registered by this call (caller

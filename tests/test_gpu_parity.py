@@ -314,6 +314,41 @@ def test_dev_batch_mixed_classes(torch_cuda):
         assert buf.cpu().numpy()[:nb].tobytes() == exp
 
 
+def test_dev_batch_plan_cache_statuses(torch_cuda):
+    """A repeated segment list reuses the device plan (no upload); statuses
+    carry a per-call epoch, so they follow each call's data and never report
+    a stale NC_ERANGE.  Uniform, grouped (3 sizes) and mapped (12 sizes)
+    classes, double -> NC_SHORT puts, outputs vs the oracle every round."""
+    import ctypes
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    ora = OracleConv()
+    rng = np.random.default_rng(12)
+    for sizes in ([4096] * 6, [4096, 10000, 4096, 777000, 10000, 4096], [1000 + 4099 * k for k in range(12)]):
+        fill = np.frombuffer(T.fill_bytes(T.NC_SHORT) + b"\0" * 8, np.uint8).copy()
+        ins = [torch.zeros(n, dtype=torch.float64, device="cuda") for n in sizes]
+        outs = [torch.zeros(n * 2 + 16, dtype=torch.uint8, device="cuda") for n in sizes]
+        arr = (pncx.Seg * len(sizes))(*[pncx.Seg(T.PNCX_PUT, 5, T.NC_SHORT, T.ITYPE_DOUBLE, n, outs[k].data_ptr(),
+                                                 ins[k].data_ptr(), fill.ctypes.data) for k, n in enumerate(sizes)])
+        st = (ctypes.c_int * len(sizes))()
+        for rnd in range(4):
+            bad = {k for k in range(len(sizes)) if (k + rnd) % 3 == 0}
+            host = []
+            for k, n in enumerate(sizes):
+                v = rng.uniform(-30000, 30000, n)
+                if k in bad:
+                    v[int(rng.integers(0, n))] = 1e9
+                ins[k].copy_(torch.from_numpy(v))
+                host.append(v)
+            torch.cuda.synchronize()
+            pncx.lib().pncx_dev_batch(arr, len(sizes), st, None)
+            torch.cuda.synchronize()
+            assert list(st) == [T.NC_ERANGE if k in bad else 0 for k in range(len(sizes))], (sizes, rnd)
+            for k, n in enumerate(sizes):
+                exp, so = ora.putn(5, T.NC_SHORT, host[k], T.ITYPE_DOUBLE, T.fill_bytes(T.NC_SHORT))
+                assert outs[k].cpu().numpy()[:n * 2].tobytes() == exp, (sizes, rnd, k)
+
+
 # ------------------------------------------- full-size (BASELINE) properties
 def _splitmix64_torch(torch, n, seed, chunk=1 << 27):
     """splitmix64 stream on the GPU (element i = mix(seed + (i+1)*golden)),
