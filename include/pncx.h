@@ -217,6 +217,65 @@ int pncx_getn_imap(int cdf_ver, int xtype, const void *xbuf, void *ibuf, int ndi
                    const pncx_offset *count, const pncx_offset *imap, int itype);
 
 /* ------------------------------------------------------------------------ */
+/* Derived user-buffer datatypes (the flexible API's bufcount + buftype).    */
+/* The reference accepts any MPI derived datatype built from one element     */
+/* type as the user-buffer layout (ncmpii_buftype_decode,                    */
+/* src/drivers/common/dtype_decode.c:628-694; NC_EMULTITYPES otherwise) and  */
+/* packs it with MPI_Pack before converting (ncmpio_pack_xbuf,               */
+/* ncmpio_util.c:620-652; MPI_Unpack after converting, :889-933).  Here the  */
+/* layout is committed once as its flattened typemap -- nblocks runs of      */
+/* blocklen[i] elements of itype at byte displacement disp[i] (any sign), in */
+/* pack order, one copy of the typemap every `extent` bytes -- and the       */
+/* pack/unpack is fused into the conversion kernel.  include/pncx_ncmpii.h   */
+/* flattens an MPI_Datatype into this form (pncx_mpi_type_commit).           */
+/* ------------------------------------------------------------------------ */
+#ifndef NC_EMULTITYPES
+#define NC_EMULTITYPES  (-208)   /* pnetcdf.h.in:629 */
+#define NC_EIOMISMATCH  (-209)   /* pnetcdf.h.in:630 */
+#endif
+typedef struct pncx_dtype pncx_dtype;
+
+/* Validate and normalise (drop empty runs, merge adjacent ones) the typemap,
+ * classify it (contiguous / uniform runs / general table) and, for a general
+ * table, upload it to HBM once so the device calls below stay asynchronous
+ * and capture-safe.  The arrays are copied.  Returns NC_NOERR, NC_EBADTYPE,
+ * NC_EINVAL, NC_ENOMEM or PNCX_EDEVICE. */
+int pncx_type_commit(int itype, pncx_offset nblocks, const pncx_offset *disp,
+                     const pncx_offset *blocklen, pncx_offset extent, pncx_dtype **dtype);
+/* Release the caller's reference; pending nonblocking requests keep theirs
+ * (MPI_Type_free semantics). */
+int pncx_type_free(pncx_dtype *dtype);
+/* itype, elements per copy, extent, and layout (0 contiguous, 1 uniform
+ * runs, 2 general table) after normalisation; any pointer may be NULL. */
+int pncx_type_inq(const pncx_dtype *dtype, int *itype, pncx_offset *nelems, pncx_offset *extent,
+                  int *layout);
+
+/* Convert prod(count[0..ndims)) elements (1 when ndims == 0) between the
+ * external buffer (contiguous, row-major over count) and a user buffer of
+ * `bufcount` copies of `buftype`, with an optional imap[] applied first
+ * (packed element index = sum idx_d*imap[d], as the reference packs the
+ * buftype and then the imap type, ncmpio_util.c:620-689).  bufcount copies
+ * must hold exactly that many elements, else NC_EIOMISMATCH
+ * (dtype_decode.c:690).  itype is the buftype's element type.  For get, the
+ * typemap must not map two elements to one address (MPI_Unpack into
+ * overlapping memory is erroneous).  Other rules as pncx_*_imap. */
+int pncx_dev_putn_flex(int cdf_ver, int xtype, void *dxbuf, const void *dbuf, int ndims,
+                       const pncx_offset *count, const pncx_offset *imap, pncx_offset bufcount,
+                       const pncx_dtype *buftype, const void *fillp, int *dstatus,
+                       pncx_stream_t stream);
+int pncx_dev_getn_flex(int cdf_ver, int xtype, const void *dxbuf, void *dbuf, int ndims,
+                       const pncx_offset *count, const pncx_offset *imap, pncx_offset bufcount,
+                       const pncx_dtype *buftype, int *dstatus, pncx_stream_t stream);
+/* host buffers: the byte span the bufcount copies cover is staged through HBM
+ * (for get it is read first, so bytes between the runs are preserved) */
+int pncx_putn_flex(int cdf_ver, int xtype, void *xbuf, const void *buf, int ndims,
+                   const pncx_offset *count, const pncx_offset *imap, pncx_offset bufcount,
+                   const pncx_dtype *buftype, const void *fillp);
+int pncx_getn_flex(int cdf_ver, int xtype, const void *xbuf, void *buf, int ndims,
+                   const pncx_offset *count, const pncx_offset *imap, pncx_offset bufcount,
+                   const pncx_dtype *buftype);
+
+/* ------------------------------------------------------------------------ */
 /* Batched conversion: many independent requests in one launch per         */
 /* conversion class (replaces the per-request loop of                       */
 /* ncmpio_igetput_varm, ncmpio_i_getput.m4:300-303, and the per-request      */

@@ -215,6 +215,34 @@ int pncx_nc_inq_buffer_usage(int ncid, pncx_offset *usage);
 int pncx_nc_bput_varm(int ncid, int varid, const pncx_offset *start, const pncx_offset *count,
                       const pncx_offset *stride, const pncx_offset *imap, const void *buf,
                       int itype, int *reqid);
+/* flexible API (ncmpi_{put,get,iput,iget}_varm[_all] with bufcount + an MPI
+ * derived buftype, dispatchers/var_getput.m4:312-382, ncmpio_getput.m4:136-
+ * 235): the user buffer is `bufcount` copies of a committed flattened
+ * buftype (pncx.h pncx_type_commit; include/pncx_ncmpii.h flattens an
+ * MPI_Datatype).  The pack/unpack runs fused into the conversion kernel.
+ * buftype NULL plays MPI_DATATYPE_NULL (bufcount ignored, the buffer holds
+ * the variable's own type).  bufcount == 0 returns NC_NOERR at once
+ * (var_getput.m4:382); an element count that differs from the request's is
+ * NC_EIOMISMATCH.  A nonblocking request keeps a reference to the buftype
+ * until it completes, so the caller may free it after posting. */
+int pncx_nc_put_varm_flex(int ncid, int varid, const pncx_offset *start, const pncx_offset *count,
+                          const pncx_offset *stride, const pncx_offset *imap, const void *buf,
+                          pncx_offset bufcount, const pncx_dtype *buftype);
+int pncx_nc_get_varm_flex(int ncid, int varid, const pncx_offset *start, const pncx_offset *count,
+                          const pncx_offset *stride, const pncx_offset *imap, void *buf,
+                          pncx_offset bufcount, const pncx_dtype *buftype);
+int pncx_nc_put_varm_flex_dev(int ncid, int varid, const pncx_offset *start, const pncx_offset *count,
+                              const pncx_offset *stride, const pncx_offset *imap, const void *dbuf,
+                              pncx_offset bufcount, const pncx_dtype *buftype, pncx_stream_t stream);
+int pncx_nc_get_varm_flex_dev(int ncid, int varid, const pncx_offset *start, const pncx_offset *count,
+                              const pncx_offset *stride, const pncx_offset *imap, void *dbuf,
+                              pncx_offset bufcount, const pncx_dtype *buftype, pncx_stream_t stream);
+int pncx_nc_iput_varm_flex(int ncid, int varid, const pncx_offset *start, const pncx_offset *count,
+                           const pncx_offset *stride, const pncx_offset *imap, const void *buf,
+                           pncx_offset bufcount, const pncx_dtype *buftype, int *reqid);
+int pncx_nc_iget_varm_flex(int ncid, int varid, const pncx_offset *start, const pncx_offset *count,
+                           const pncx_offset *stride, const pncx_offset *imap, void *buf,
+                           pncx_offset bufcount, const pncx_dtype *buftype, int *reqid);
 /* nreqs == NC_REQ_ALL / NC_PUT_REQ_ALL / NC_GET_REQ_ALL: every pending (put/get) request */
 int pncx_nc_wait_all(int ncid, int nreqs, int *reqids, int *statuses);
 int pncx_nc_cancel(int ncid, int nreqs, int *reqids, int *statuses);

@@ -724,6 +724,282 @@ int pncx_getn_imap(int cdf_ver, int xtype, const void *xbuf, void *ibuf, int ndi
 }
 
 /* ------------------------------------------------------------------------ */
+/* derived buftypes: committed flattened typemaps, pack/unpack fused into    */
+/* the imap gather/scatter kernel (pncx_kern.hpp tmap_byte)                  */
+/* ------------------------------------------------------------------------ */
+struct pncx_dtype {
+    int        itype, isz, layout;
+    int        refs;
+    long long  tn, extent, nblk;
+    long long  lo, hi;                /* byte bounds of one copy: [lo, hi)     */
+    long long  len, stride, disp0;    /* layout 0/1                            */
+    long long *pre, *disp;            /* host table (nblk each)                */
+    long long *dtab;                  /* device: pre[nblk] then disp[nblk]     */
+};
+
+int pncx_type_commit(int itype, pncx_offset nblocks, const pncx_offset *disp,
+                     const pncx_offset *blocklen, pncx_offset extent, pncx_dtype **dtype)
+{
+    pncx_dtype *t;
+    long long i, k = 0, *len;
+    const int isz = pncx_ilen(itype);
+    if (dtype == NULL) return NC_EINVAL;
+    *dtype = NULL;
+    if (isz < 0) return NC_EBADTYPE;
+    if (nblocks < 0 || (nblocks > 0 && (disp == NULL || blocklen == NULL))) return NC_EINVAL;
+    for (i = 0; i < nblocks; i++)
+        if (blocklen[i] < 0) return NC_EINVAL;
+    t = (pncx_dtype *)calloc(1, sizeof *t);
+    len = (long long *)malloc(sizeof(long long) * (size_t)(nblocks ? nblocks : 1));
+    if (t != NULL) {
+        t->pre = (long long *)malloc(sizeof(long long) * (size_t)(nblocks ? nblocks : 1));
+        t->disp = (long long *)malloc(sizeof(long long) * (size_t)(nblocks ? nblocks : 1));
+    }
+    if (t == NULL || len == NULL || t->pre == NULL || t->disp == NULL) {
+        if (t) { free(t->pre); free(t->disp); }
+        free(t);
+        free(len);
+        return NC_ENOMEM;
+    }
+    t->itype = itype;
+    t->isz = isz;
+    t->extent = extent;
+    t->refs = 1;
+    /* normalise: drop empty runs, merge runs that continue each other */
+    for (i = 0; i < nblocks; i++) {
+        if (blocklen[i] == 0) continue;
+        if (k > 0 && t->disp[k - 1] + len[k - 1] * isz == disp[i]) { len[k - 1] += blocklen[i]; continue; }
+        t->disp[k] = disp[i];
+        len[k++] = blocklen[i];
+    }
+    t->nblk = k;
+    for (i = 0; i < k; i++) {
+        const long long end = t->disp[i] + len[i] * isz;
+        t->pre[i] = t->tn;
+        t->tn += len[i];
+        if (i == 0 || t->disp[i] < t->lo) t->lo = t->disp[i];
+        if (i == 0 || end > t->hi) t->hi = end;
+    }
+    if (k == 0 || (k == 1 && extent == len[0] * isz)) {
+        t->layout = 0;                                   /* contiguous */
+        t->disp0 = k ? t->disp[0] : 0;
+        t->len = k ? len[0] : 0;
+    } else {
+        int uniform = 1;
+        for (i = 1; i < k && uniform; i++)
+            uniform = len[i] == len[0] && t->disp[i] - t->disp[i - 1] == t->disp[1] - t->disp[0];
+        t->len = len[0];
+        t->disp0 = t->disp[0];
+        t->stride = k > 1 ? t->disp[1] - t->disp[0] : 0;
+        t->layout = uniform ? 1 : 2;
+    }
+    free(len);
+    if (t->layout == 2 && have_device()) {
+        /* the general table lives in HBM from now on: device calls stay async */
+        const size_t tb = sizeof(long long) * (size_t)k;
+        if (pncxrt_malloc((void **)&t->dtab, 2 * tb) != 0 ||
+            pncxrt_memcpy_h2d(t->dtab, t->pre, tb, NULL) != 0 ||
+            pncxrt_memcpy_h2d(t->dtab + k, t->disp, tb, NULL) != 0 ||
+            pncxrt_stream_sync(NULL) != 0) {
+            pncxrt_free(t->dtab);
+            free(t->pre);
+            free(t->disp);
+            free(t);
+            return PNCX_EDEVICE;
+        }
+    }
+    *dtype = t;
+    return NC_NOERR;
+}
+
+/* reference counting: requests that hold a dtype until wait use these */
+pncx_dtype *pncx_type_ref(pncx_dtype *t)
+{
+    if (t) __atomic_add_fetch(&t->refs, 1, __ATOMIC_ACQ_REL);
+    return t;
+}
+
+int pncx_type_free(pncx_dtype *t)
+{
+    if (t == NULL) return NC_EINVAL;
+    if (__atomic_sub_fetch(&t->refs, 1, __ATOMIC_ACQ_REL) > 0) return NC_NOERR;
+    if (t->dtab) {
+        pncxrt_stream_sync(NULL);
+        pncxrt_free(t->dtab);
+    }
+    free(t->pre);
+    free(t->disp);
+    free(t);
+    return NC_NOERR;
+}
+
+/* 1 when bufcount copies of t are one contiguous run, starting *lo bytes in */
+int pncx_type_contig(const pncx_dtype *t, long long bufcount, long long *lo)
+{
+    *lo = t->nblk ? t->disp0 : 0;
+    return t->layout == 0 || (t->nblk == 1 && bufcount == 1);
+}
+
+int pncx_type_inq(const pncx_dtype *t, int *itype, pncx_offset *nelems, pncx_offset *extent, int *layout)
+{
+    if (t == NULL) return NC_EINVAL;
+    if (itype) *itype = t->itype;
+    if (nelems) *nelems = t->tn;
+    if (extent) *extent = t->extent;
+    if (layout) *layout = t->layout;
+    return NC_NOERR;
+}
+
+/*
+ * Layout of one flexible call.  Returns 0 when the bufcount copies are one
+ * contiguous run starting *base bytes after buf (then the plain / imap kernels
+ * apply), 1 when the fused typemap kernel is needed (m filled, user bytes in
+ * [*lo, *hi) relative to buf), -1 with *err set on a bad argument.
+ */
+static int flex_layout(int ndims, const pncx_offset *count, const pncx_offset *imap, long long bufcount,
+                       const pncx_dtype *t, pncxk_imap *m, long long *n, long long *lo, long long *hi,
+                       int *err)
+{
+    long long span;
+    *lo = *hi = 0;
+    if (t == NULL || bufcount < 0) { *err = NC_EINVAL; return -1; }
+    if (!imap_layout(ndims, count, imap, m, n, &span, err)) {
+        if (*err != NC_NOERR) return -1;
+        m->ndims = 1;                     /* packed order: offset = k */
+        m->count[0] = *n;
+        m->imap[0] = 1;
+        m->max_count = *n;
+    }
+    if (bufcount * t->tn != *n) { *err = NC_EIOMISMATCH; return -1; }   /* dtype_decode.c:690 */
+    if (t->layout == 0 || (t->nblk == 1 && bufcount == 1)) {
+        *lo = t->nblk ? t->disp0 : 0;
+        return 0;
+    }
+    m->tmode = t->layout;
+    m->tn = t->tn;
+    m->textent = t->extent;
+    m->tlen = t->len;
+    m->tstride = t->stride;
+    m->tdisp0 = t->disp0;
+    m->tnblk = t->nblk;
+    m->tpre = t->dtab;
+    m->tdisp = t->dtab ? t->dtab + t->nblk : NULL;
+    {
+        const long long last = (bufcount - 1) * t->extent;
+        *lo = t->lo < last + t->lo ? t->lo : last + t->lo;
+        *hi = t->hi > last + t->hi ? t->hi : last + t->hi;
+    }
+    return 1;
+}
+
+int pncx_dev_putn_flex(int cdf_ver, int xtype, void *dxbuf, const void *dbuf, int ndims,
+                       const pncx_offset *count, const pncx_offset *imap, pncx_offset bufcount,
+                       const pncx_dtype *bt, const void *fillp, int *dstatus, pncx_stream_t stream)
+{
+    op_t op;
+    pncxk_imap m;
+    long long n, lo, hi;
+    int err, r;
+    if (bt == NULL) return NC_EINVAL;
+    if ((err = classify(PNCX_PUT, cdf_ver, xtype, bt->itype, fillp, &op)) != NC_NOERR) return err;
+    if ((r = flex_layout(ndims, count, imap, bufcount, bt, &m, &n, &lo, &hi, &err)) < 0) return err;
+    if (r == 0)
+        return pncx_dev_putn_imap(cdf_ver, xtype, dxbuf, (const char *)dbuf + lo, ndims, count, imap,
+                                  bt->itype, fillp, dstatus, stream);
+    if (n <= 0) return NC_NOERR;
+    if (!have_device() || (m.tmode == 2 && m.tpre == NULL)) return PNCX_EDEVICE;
+    return launch_imap_op(&op, dbuf, dxbuf, n, &m, 1, dstatus, stream);
+}
+
+int pncx_dev_getn_flex(int cdf_ver, int xtype, const void *dxbuf, void *dbuf, int ndims,
+                       const pncx_offset *count, const pncx_offset *imap, pncx_offset bufcount,
+                       const pncx_dtype *bt, int *dstatus, pncx_stream_t stream)
+{
+    op_t op;
+    pncxk_imap m;
+    long long n, lo, hi;
+    int err, r;
+    if (bt == NULL) return NC_EINVAL;
+    if ((err = classify(PNCX_GET, cdf_ver, xtype, bt->itype, NULL, &op)) != NC_NOERR) return err;
+    if ((r = flex_layout(ndims, count, imap, bufcount, bt, &m, &n, &lo, &hi, &err)) < 0) return err;
+    if (r == 0)
+        return pncx_dev_getn_imap(cdf_ver, xtype, dxbuf, (char *)dbuf + lo, ndims, count, imap,
+                                  bt->itype, dstatus, stream);
+    if (n <= 0) return NC_NOERR;
+    if (!have_device() || (m.tmode == 2 && m.tpre == NULL)) return PNCX_EDEVICE;
+    return launch_imap_op(&op, dxbuf, dbuf, n, &m, 0, dstatus, stream);
+}
+
+/* host buffers: stage the user byte span [lo, hi) and the packed buffer */
+static int host_flex(int dir, int cdf_ver, int xtype, void *xbuf, void *buf, int ndims,
+                     const pncx_offset *count, const pncx_offset *imap, long long bufcount,
+                     const pncx_dtype *bt, const void *fillp)
+{
+    op_t op;
+    pncxk_imap m;
+    long long n, lo, hi;
+    ctx_t *c;
+    int err, r, st = 0;
+    pinned_t pn = {{NULL, NULL}, 0};
+    size_t xs, xb, ub;
+    uint8_t *dx, *du, *ubase;
+    void *s;
+    if (bt == NULL) return NC_EINVAL;
+    if ((err = classify(dir, cdf_ver, xtype, bt->itype, fillp, &op)) != NC_NOERR) return err;
+    if ((r = flex_layout(ndims, count, imap, bufcount, bt, &m, &n, &lo, &hi, &err)) < 0) return err;
+    if (r == 0)
+        return dir == PNCX_PUT
+                   ? pncx_putn_imap(cdf_ver, xtype, xbuf, (const char *)buf + lo, ndims, count, imap, bt->itype, fillp)
+                   : pncx_getn_imap(cdf_ver, xtype, xbuf, (char *)buf + lo, ndims, count, imap, bt->itype);
+    if (n <= 0) return NC_NOERR;
+    if (!have_device() || (m.tmode == 2 && m.tpre == NULL)) return PNCX_EDEVICE;
+    c = get_ctx();
+    if (c == NULL) return PNCX_EDEVICE;
+    xs = (size_t)pncx_xlen(xtype);
+    xb = ALIGN16((size_t)n * xs);
+    ub = (size_t)(hi - lo);
+    ubase = (uint8_t *)buf + lo;
+    pthread_mutex_lock(&c->lock);
+    pin_range(&pn, ubase, ub);
+    pin_range(&pn, xbuf, (size_t)n * xs);
+    s = c->stream[0];
+    err = ensure_dbuf(c, xb + ALIGN16(ub));
+    dx = (uint8_t *)c->dbuf[0];
+    du = dx + xb;
+    if (!err) err = pncxrt_memset(c->dstatus, 0, sizeof(int), s);
+    if (!err) err = pncxrt_memcpy_h2d(du, ubase, ub, s);       /* user span (get: keeps the holes) */
+    if (dir == PNCX_PUT) {
+        if (!err && op.c) err = pncxrt_memcpy_h2d(dx, xbuf, (size_t)n * xs, s);
+        if (!err) err = launch_imap_op(&op, du - lo, dx, n, &m, 1, c->dstatus, s);
+        if (!err) err = pncxrt_memcpy_d2h(xbuf, dx, (size_t)n * xs, s);
+    } else {
+        if (!err) err = pncxrt_memcpy_h2d(dx, xbuf, (size_t)n * xs, s);
+        if (!err) err = launch_imap_op(&op, dx, du - lo, n, &m, 0, c->dstatus, s);
+        if (!err) err = pncxrt_memcpy_d2h(ubase, du, ub, s);
+    }
+    if (!err) err = pncxrt_memcpy_d2h(&st, c->dstatus, sizeof(int), s);
+    if (!err) err = pncxrt_stream_sync(s);
+    unpin_all(&pn);
+    pthread_mutex_unlock(&c->lock);
+    if (err) return err < 0 ? err : PNCX_EDEVICE;
+    return st;
+}
+
+int pncx_putn_flex(int cdf_ver, int xtype, void *xbuf, const void *buf, int ndims,
+                   const pncx_offset *count, const pncx_offset *imap, pncx_offset bufcount,
+                   const pncx_dtype *bt, const void *fillp)
+{
+    return host_flex(PNCX_PUT, cdf_ver, xtype, xbuf, (void *)buf, ndims, count, imap, bufcount, bt, fillp);
+}
+
+int pncx_getn_flex(int cdf_ver, int xtype, const void *xbuf, void *buf, int ndims,
+                   const pncx_offset *count, const pncx_offset *imap, pncx_offset bufcount,
+                   const pncx_dtype *bt)
+{
+    return host_flex(PNCX_GET, cdf_ver, xtype, (void *)xbuf, buf, ndims, count, imap, bufcount, bt, NULL);
+}
+
+/* ------------------------------------------------------------------------ */
 /* batched                                                                   */
 /* ------------------------------------------------------------------------ */
 typedef struct bitem_t {

@@ -423,6 +423,27 @@ __device__ __forceinline__ int64_t imap_offset(IDX k, const pncxk_imap &m) {
     return off + (int64_t)k * m.imap[0];
 }
 
+// Byte offset of packed element j of a flattened derived buftype (the typemap
+// MPI_Pack walks, dtype_decode.c:628-694 + ncmpio_util.c:620-652): copy
+// c = j / tn, element r = j % tn inside it, found in block b by a binary search
+// over the block prefix (tmode 2) or by a divide (uniform blocks, tmode 1).
+template <int ES>
+__device__ __forceinline__ int64_t tmap_byte(int64_t j, const pncxk_imap &m) {
+    const int64_t c = j / m.tn;
+    const int64_t r = j - c * m.tn;
+    if (m.tmode == 1) {
+        const int64_t q = r / m.tlen;
+        return c * m.textent + m.tdisp0 + q * m.tstride + (r - q * m.tlen) * ES;
+    }
+    int64_t lo = 0, hi = m.tnblk - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (m.tpre[mid] <= r) lo = mid;
+        else hi = mid - 1;
+    }
+    return c * m.textent + m.tdisp[lo] + (r - m.tpre[lo]) * ES;
+}
+
 // GATHER = true: src strided (user, put); false: dst strided (user, get)
 template <class Op, bool GATHER, typename IDX>
 __global__ __launch_bounds__(256) void k_imap(const uint8_t *src, uint8_t *dst, int64_t n, pncxk_imap m,
@@ -433,8 +454,15 @@ __global__ __launch_bounds__(256) void k_imap(const uint8_t *src, uint8_t *dst, 
     bool bad = false;
     for (int64_t k = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 + threadIdx.x; k < n; k += stride) {
         const int64_t u = imap_offset<IDX>((IDX)k, m);          // user element offset
-        const uint8_t *ps = src + (GATHER ? u : k) * Op::SS;
-        uint8_t *pd = dst + (GATHER ? k : u) * Op::DS;
+        const uint8_t *ps;
+        uint8_t *pd;
+        if constexpr (GATHER) {
+            ps = src + (m.tmode ? tmap_byte<Op::SS>(u, m) : u * Op::SS);
+            pd = dst + k * Op::DS;
+        } else {
+            ps = src + k * Op::SS;
+            pd = dst + (m.tmode ? tmap_byte<Op::DS>(u, m) : u * Op::DS);
+        }
         const SU s = ld_unaligned<SU>(ps);
         DU old = 0;
         if constexpr (Op::PRESERVE) old = ld_unaligned<DU>(pd);

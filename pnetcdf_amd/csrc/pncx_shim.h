@@ -65,6 +65,18 @@ typedef struct pncxk_imap {
     long long max_count;
     long long count[PNCX_MAX_DIMS];
     long long imap[PNCX_MAX_DIMS];   /* in elements of the internal type */
+    /* flattened user-buffer datatype applied after imap (the MPI_Pack
+     * typemap of a derived buftype): the imap offset j is the packed
+     * element index; copy c = j / tn sits textent bytes after copy c-1.
+     * tmode 0: none, byte offset = j * element size
+     *       1: uniform blocks of tlen elements, tstride bytes apart from tdisp0
+     *       2: table, tnblk blocks, tpre[b] = first packed element of block b,
+     *          tdisp[b] = its byte displacement (device arrays) */
+    int       tmode;
+    int       tpad;
+    long long tn, textent, tlen, tstride, tdisp0, tnblk;
+    const long long *tpre;
+    const long long *tdisp;
 } pncxk_imap;
 
 typedef struct pncxk_opinfo {

@@ -29,7 +29,7 @@ ERR = dict(
     NC_ENOTVAR=-49, NC_EGLOBAL=-50, NC_ENOTNC=-51, NC_EMAXNAME=-53, NC_EUNLIMIT=-54, NC_ECHAR=-56,
     NC_EEDGE=-57, NC_ESTRIDE=-58, NC_EBADNAME=-59, NC_ERANGE=-60, NC_ENOMEM=-61, NC_EVARSIZE=-62,
     NC_EDIMSIZE=-63, NC_ENOTNC3=-113, NC_ENOTBUILT=-128, NC_ENULLPAD=-134, NC_EFILE=-204,
-    NC_EREAD=-205, NC_EWRITE=-206, NC_ENEGATIVECNT=-210, NC_EINVAL_REQUEST=-212, NC_EPREVATTACHBUF=-216,
+    NC_EREAD=-205, NC_EWRITE=-206, NC_EMULTITYPES=-208, NC_EIOMISMATCH=-209, NC_ENEGATIVECNT=-210, NC_EINVAL_REQUEST=-212, NC_EPREVATTACHBUF=-216,
     NC_ENULLABUF=-217, NC_EPENDINGBPUT=-218, NC_EINSUFFBUF=-219, NC_ENOENT=-220,
     NC_EINTOVERFLOW=-221, NC_ENULLSTART=-226, NC_EINVAL_CMODE=-228, NC_ESTRICTCDF2=-232, NC_ENOTRECVAR=-233,
     NC_ENOTFILL=-234, NC_EINVAL_OMODE=-235, NC_EPENDING=-236, PNCX_EDEVICE=-1900)
@@ -84,6 +84,12 @@ def lib():
         "pncx_nc_buffer_attach": [i, ll], "pncx_nc_buffer_detach": [i],
         "pncx_nc_inq_buffer_size": [i, lp], "pncx_nc_inq_buffer_usage": [i, lp],
         "pncx_nc_bput_varm": [i, i, vp, vp, vp, vp, vp, i, ip],
+        "pncx_nc_put_varm_flex": [i, i, vp, vp, vp, vp, vp, ll, vp],
+        "pncx_nc_get_varm_flex": [i, i, vp, vp, vp, vp, vp, ll, vp],
+        "pncx_nc_put_varm_flex_dev": [i, i, vp, vp, vp, vp, vp, ll, vp, vp],
+        "pncx_nc_get_varm_flex_dev": [i, i, vp, vp, vp, vp, vp, ll, vp, vp],
+        "pncx_nc_iput_varm_flex": [i, i, vp, vp, vp, vp, vp, ll, vp, ip],
+        "pncx_nc_iget_varm_flex": [i, i, vp, vp, vp, vp, vp, ll, vp, ip],
         "pncx_nc_put_varn": [i, i, i, vp, vp, vp, i], "pncx_nc_get_varn": [i, i, i, vp, vp, vp, i],
         "pncx_nc_iput_varn": [i, i, i, vp, vp, vp, i, ip], "pncx_nc_iget_varn": [i, i, i, vp, vp, vp, i, ip],
     }
@@ -399,6 +405,56 @@ def iget_var(ncid, varid, out, start=None, count=None, stride=None, imap=None, i
     it = itype if itype is not None else itype_of(out)
     r = ctypes.c_int(NC_REQ_NULL)
     err = lib().pncx_nc_iget_varm(ncid, varid, *a, out.ctypes.data if out.size else None, it, ctypes.byref(r))
+    return err, r.value
+
+
+# flexible API: buf holds `bufcount` copies of `buftype` (a pncx.DType, or
+# None for MPI_DATATYPE_NULL) starting `base` bytes into the numpy/torch buffer
+def _h(buftype):
+    return None if buftype is None else buftype.handle
+
+
+def put_var_flex(ncid, varid, buf, bufcount, buftype, start=None, count=None, stride=None, imap=None, base=0):
+    keep, a = _args(start, count, stride, imap)
+    return lib().pncx_nc_put_varm_flex(ncid, varid, *a, buf.ctypes.data + base, bufcount, _h(buftype))
+
+
+def get_var_flex(ncid, varid, out, bufcount, buftype, start=None, count=None, stride=None, imap=None, base=0):
+    keep, a = _args(start, count, stride, imap)
+    return lib().pncx_nc_get_varm_flex(ncid, varid, *a, out.ctypes.data + base, bufcount, _h(buftype))
+
+
+def put_var_flex_dev(ncid, varid, t, bufcount, buftype, start=None, count=None, stride=None, imap=None, base=0,
+                     stream=None):
+    import torch
+    keep, a = _args(start, count, stride, imap)
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return lib().pncx_nc_put_varm_flex_dev(ncid, varid, *a, t.data_ptr() + base, bufcount, _h(buftype),
+                                           ctypes.c_void_p(s.cuda_stream))
+
+
+def get_var_flex_dev(ncid, varid, t, bufcount, buftype, start=None, count=None, stride=None, imap=None, base=0,
+                     stream=None):
+    import torch
+    keep, a = _args(start, count, stride, imap)
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return lib().pncx_nc_get_varm_flex_dev(ncid, varid, *a, t.data_ptr() + base, bufcount, _h(buftype),
+                                           ctypes.c_void_p(s.cuda_stream))
+
+
+def iput_var_flex(ncid, varid, buf, bufcount, buftype, start=None, count=None, stride=None, imap=None, base=0):
+    keep, a = _args(start, count, stride, imap)
+    r = ctypes.c_int(NC_REQ_NULL)
+    err = lib().pncx_nc_iput_varm_flex(ncid, varid, *a, buf.ctypes.data + base, bufcount, _h(buftype),
+                                       ctypes.byref(r))
+    return err, r.value
+
+
+def iget_var_flex(ncid, varid, out, bufcount, buftype, start=None, count=None, stride=None, imap=None, base=0):
+    keep, a = _args(start, count, stride, imap)
+    r = ctypes.c_int(NC_REQ_NULL)
+    err = lib().pncx_nc_iget_varm_flex(ncid, varid, *a, out.ctypes.data + base, bufcount, _h(buftype),
+                                       ctypes.byref(r))
     return err, r.value
 
 

@@ -11,6 +11,7 @@ NC_UBYTE, NC_USHORT, NC_UINT, NC_INT64, NC_UINT64 = 7, 8, 9, 10, 11
 
 NC_NOERR, NC_EINVAL, NC_EBADTYPE, NC_ECHAR, NC_ERANGE, NC_ENOMEM = 0, -36, -45, -56, -60, -61
 PNCX_EDEVICE = -1900
+NC_EMULTITYPES, NC_EIOMISMATCH = -208, -209   # pnetcdf.h.in:629-630
 
 # internal types (enum pncx_itype)
 ITYPE_SCHAR, ITYPE_UCHAR, ITYPE_SHORT, ITYPE_USHORT, ITYPE_INT, ITYPE_UINT = 1, 2, 3, 4, 5, 6

@@ -58,6 +58,13 @@ def lib():
         "pncx_putn_imap": (i, [i, i, vp, vp, i, vp, vp, i, vp]),
         "pncx_getn_imap": (i, [i, i, vp, vp, i, vp, vp, i]),
         "pncx_batch": (i, [vp, i, vp]),
+        "pncx_type_commit": (i, [i, ll, vp, vp, ll, vp]),
+        "pncx_type_free": (i, [vp]),
+        "pncx_type_inq": (i, [vp, vp, vp, vp, vp]),
+        "pncx_putn_flex": (i, [i, i, vp, vp, i, vp, vp, ll, vp, vp]),
+        "pncx_getn_flex": (i, [i, i, vp, vp, i, vp, vp, ll, vp]),
+        "pncx_dev_putn_flex": (i, [i, i, vp, vp, i, vp, vp, ll, vp, vp, vp, vp]),
+        "pncx_dev_getn_flex": (i, [i, i, vp, vp, i, vp, vp, ll, vp, vp, vp]),
         "pncx_dev_fill": (i, [i, vp, ll, vp, vp]),
         "pncx_fill": (i, [i, vp, ll, vp]),
         "pncx_device_count": (i, []), "pncx_set_device": (i, [i]),
@@ -200,6 +207,83 @@ def dev_getn_imap(cdf_ver, xtype, dx, di, count, imap, itype, dstatus=None, stre
     _check(lib().pncx_dev_getn_imap(cdf_ver, xtype, _dptr(dx), _dptr(di), len(c), cp, mp, itype,
                                     None if dstatus is None else _dptr(dstatus), _stream_ptr(stream)),
            "dev_getn_imap", (T.NC_NOERR,))
+
+
+class DType:
+    """A committed derived user-buffer datatype (pncx_type_commit): runs of
+    blocklen[i] elements of itype at byte displacement disp[i], in pack
+    order, one copy every `extent` bytes -- the flattened typemap of an MPI
+    derived buftype (dtype_decode.c:628-694)."""
+
+    def __init__(self, itype, disp, blocklen, extent):
+        d, dp = _offs(disp)
+        b, bp = _offs(blocklen)
+        h = ctypes.c_void_p()
+        _check(lib().pncx_type_commit(itype, len(d), dp, bp, extent, ctypes.byref(h)), "type_commit",
+               (T.NC_NOERR,))
+        self.handle = h
+        self.itype = itype
+
+    def inq(self):
+        it, n, ext, lay = ctypes.c_int(), ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_int()
+        _check(lib().pncx_type_inq(self.handle, ctypes.byref(it), ctypes.byref(n), ctypes.byref(ext),
+                                   ctypes.byref(lay)), "type_inq", (T.NC_NOERR,))
+        return {"itype": it.value, "nelems": n.value, "extent": ext.value, "layout": lay.value}
+
+    def free(self):
+        if self.handle:
+            lib().pncx_type_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def _fill_arg(fillp):
+    fb = None if fillp is None else np.frombuffer(bytes(fillp) + b"\0" * 8, np.uint8).copy()
+    return fb, (None if fb is None else _np_ptr(fb))
+
+
+def putn_flex(cdf_ver, xtype, xbuf, buf, count, imap, bufcount, dtype, fillp=None, base=0):
+    """put with a derived buftype: `buf` (numpy bytes) holds bufcount copies
+    of dtype starting `base` bytes in (displacements may be negative)."""
+    c, cp = _offs(count)
+    mp = None if imap is None else _offs(imap)
+    fb, fbp = _fill_arg(fillp)
+    return _check(lib().pncx_putn_flex(cdf_ver, xtype, _np_ptr(xbuf), ctypes.c_void_p(buf.ctypes.data + base),
+                                       len(c), cp, None if mp is None else mp[1], bufcount, dtype.handle, fbp),
+                  "putn_flex")
+
+
+def getn_flex(cdf_ver, xtype, xbuf, buf, count, imap, bufcount, dtype, base=0):
+    c, cp = _offs(count)
+    mp = None if imap is None else _offs(imap)
+    return _check(lib().pncx_getn_flex(cdf_ver, xtype, _np_ptr(xbuf), ctypes.c_void_p(buf.ctypes.data + base),
+                                       len(c), cp, None if mp is None else mp[1], bufcount, dtype.handle),
+                  "getn_flex")
+
+
+def dev_putn_flex(cdf_ver, xtype, dx, dbuf, count, imap, bufcount, dtype, fillp=None, dstatus=None,
+                  stream=None, base=0):
+    c, cp = _offs(count)
+    mp = None if imap is None else _offs(imap)
+    fb, fbp = _fill_arg(fillp)
+    _check(lib().pncx_dev_putn_flex(cdf_ver, xtype, _dptr(dx), ctypes.c_void_p(dbuf.data_ptr() + base), len(c),
+                                    cp, None if mp is None else mp[1], bufcount, dtype.handle, fbp,
+                                    None if dstatus is None else _dptr(dstatus), _stream_ptr(stream)),
+           "dev_putn_flex", (T.NC_NOERR,))
+
+
+def dev_getn_flex(cdf_ver, xtype, dx, dbuf, count, imap, bufcount, dtype, dstatus=None, stream=None, base=0):
+    c, cp = _offs(count)
+    mp = None if imap is None else _offs(imap)
+    _check(lib().pncx_dev_getn_flex(cdf_ver, xtype, _dptr(dx), ctypes.c_void_p(dbuf.data_ptr() + base), len(c),
+                                    cp, None if mp is None else mp[1], bufcount, dtype.handle,
+                                    None if dstatus is None else _dptr(dstatus), _stream_ptr(stream)),
+           "dev_getn_flex", (T.NC_NOERR,))
 
 
 def batch(segs):

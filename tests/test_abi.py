@@ -18,6 +18,7 @@ from pnetcdf_amd import nctypes as T
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "pnetcdf_amd", "lib", "libpncx.so")
 LIB_MPI = os.path.join(ROOT, "pnetcdf_amd", "lib", "libpncx_ncmpii.so")
+LIB_MPIDT = os.path.join(ROOT, "pnetcdf_amd", "lib", "libpncx_mpi.so")
 
 
 def declared(header):
@@ -35,14 +36,14 @@ def exported(lib):
 
 @pytest.fixture(scope="module")
 def built():
-    if not os.path.exists(LIB) or not os.path.exists(LIB_MPI):
+    if not all(os.path.exists(p) for p in (LIB, LIB_MPI, LIB_MPIDT)):
         subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "pnetcdf_amd", "csrc")], check=True)
     return True
 
 
 def test_pncx_h_symbols_exported(built):
     decl = declared("pncx.h")
-    assert len(decl) == 27
+    assert len(decl) == 34
     missing = [s for s in decl if s not in exported(LIB)]
     assert not missing, missing
 
@@ -50,7 +51,7 @@ def test_pncx_h_symbols_exported(built):
 def test_pncx_nc_h_symbols_exported(built):
     """file-level API (include/pncx_nc.h)"""
     decl = declared("pncx_nc.h")
-    assert len(decl) == 53
+    assert len(decl) == 59
     missing = [s for s in decl if s not in exported(LIB)]
     assert not missing, missing
 
@@ -62,6 +63,15 @@ def test_ncmpii_symbols_exported(built):
             "ncmpii_getn_NC_INT", "ncmpii_putn_NC_BYTE", "ncmpii_getn_NC_UINT64"} <= set(decl)
     assert len([d for d in decl if d.startswith("ncmpii_")]) == 24
     missing = [s for s in decl if s not in exported(LIB_MPI)]
+    assert not missing, missing
+
+
+def test_mpi_buftype_symbols_exported(built):
+    """flexible API over MPI derived datatypes (include/pncx_mpi.h)"""
+    decl = declared("pncx_mpi.h")
+    assert set(decl) == {"pncx_mpi_type_flatten", "pncx_mpi_type_commit", "pncx_ncmpi_put_varm",
+                         "pncx_ncmpi_get_varm", "pncx_ncmpi_iput_varm", "pncx_ncmpi_iget_varm"}
+    missing = [s for s in decl if s not in exported(LIB_MPIDT)]
     assert not missing, missing
 
 

@@ -1,0 +1,173 @@
+"""Derived user-buffer datatypes (flexible API) vs numpy pack + the CPU oracle (GPU).
+
+Reference semantics (ncmpio_pack_xbuf, ncmpio_util.c:620-689, 716-765; unpack
+:842-966): MPI_Pack the bufcount copies of the buftype into a contiguous lbuf,
+then the imap type, then convert; for get, convert then MPI_Unpack (bytes of
+the user buffer between the runs are untouched).  The typemap model here is
+numpy: element k of copy c sits at c*extent + disp[b] + (k - pre[b])*isize.
+The kernels fuse that gather/scatter into the conversion (pncx_kern.hpp
+tmap_byte).  The MPI side (flattening real MPI datatypes, and the whole
+flexible file path vs MPI_Pack/Unpack) is tests/mpi/flex_check.c.
+"""
+import os
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+
+from pnetcdf_amd import nctypes as T
+from tests.converters import OracleConv
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def elem_offsets(disp, blocklen, extent, bufcount, isz):
+    """byte offset of every packed element (MPI_Pack order)"""
+    one = np.concatenate([d + isz * np.arange(b, dtype=np.int64) for d, b in zip(disp, blocklen)]
+                         or [np.zeros(0, np.int64)])
+    return (np.arange(bufcount, dtype=np.int64)[:, None] * extent + one[None, :]).reshape(-1)
+
+
+def imap_offsets(count, imap):
+    idx = np.indices(count).reshape(len(count), -1)
+    return (idx * np.asarray(imap, np.int64)[:, None]).sum(0)
+
+
+# (name, disp in elements, blocklen, extent in elements, bufcount) -- layout the commit must pick
+TYPES = [
+    ("vector", [0, 4, 8], [2, 2, 2], 12, 2, 1),
+    ("indexed_irregular", [7, 0, 11, 3], [2, 1, 3, 1], 14, 2, 2),
+    ("contig_offset", [3], [10], 10, 3, 0),
+    ("negative_disp", [4, -2, 9], [2, 1, 2], 12, 1, 2),
+    ("single_block_resized", [0], [3], 7, 4, 1),
+    ("runs_merge", [0, 2, 5], [2, 3, 1], 9, 2, 1),     # the three runs merge into one: uniform
+    ("descending", [9, 6, 3, 0], [1, 1, 1, 1], 10, 3, 1),
+]
+PAIRS = [(T.NC_INT, T.ITYPE_INT), (T.NC_FLOAT, T.ITYPE_DOUBLE), (T.NC_SHORT, T.ITYPE_INT),
+         (T.NC_DOUBLE, T.ITYPE_DOUBLE), (T.NC_BYTE, T.ITYPE_SCHAR), (T.NC_INT64, T.ITYPE_LONGLONG),
+         (T.NC_UBYTE, T.ITYPE_FLOAT)]
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def user_values(rng, it, nbytes):
+    isz = T.ilen(it)
+    n = nbytes // isz
+    if np.issubdtype(np.dtype(T.ITYPE_NP[it]), np.floating):
+        v = (rng.standard_normal(n) * 4e4).astype(T.ITYPE_NP[it])
+    else:
+        v = np.frombuffer(rng.integers(0, 256, n * isz, dtype=np.uint8).tobytes(), T.ITYPE_NP[it]).copy()
+        if isz >= 4:
+            v = (v % 70000 - 35000).astype(T.ITYPE_NP[it])    # some out of range for NC_SHORT
+    return v.view(np.uint8)
+
+
+def run_case(torch, where, xt, it, disp_el, blocklen, ext_el, bufcount, count, imap, seed):
+    from pnetcdf_amd import pncx
+    ora = OracleConv()
+    rng = np.random.default_rng(seed)
+    isz, xsz = T.ilen(it), T.xlen(xt)
+    disp = [d * isz for d in disp_el]
+    offs = elem_offsets(disp, blocklen, ext_el * isz, bufcount, isz)
+    lo = int(offs.min()) if offs.size else 0
+    hi = int(offs.max()) + isz if offs.size else 0
+    base = -lo + 16                                       # buffer origin inside the array
+    ub = user_values(rng, it, base + hi + 16)
+    n = offs.size
+    if count is None:
+        count, imap = [n], None
+    jm = np.arange(n) if imap is None else imap_offsets(count, imap)
+    src = (base + offs[jm])[:, None] + np.arange(isz)[None, :]
+    packed = ub[src.reshape(-1)].view(T.ITYPE_NP[it])
+    fill = T.fill_bytes(xt, 42)
+    exp_x, exp_st = ora.putn(5, xt, packed, it, fill)
+    dt = pncx.DType(it, disp, blocklen, ext_el * isz)
+    # ---- put
+    if where == "host":
+        xb = np.zeros(n * xsz, np.uint8)
+        st = pncx.putn_flex(5, xt, xb, ub, count, imap, bufcount, dt, fill, base=base)
+        got_x = xb.tobytes()
+    else:
+        du = torch.from_numpy(ub.copy()).cuda()
+        dx = torch.zeros(max(n * xsz, 16), dtype=torch.uint8, device="cuda")
+        ds = torch.zeros(1, dtype=torch.int32, device="cuda")
+        pncx.dev_putn_flex(5, xt, dx, du, count, imap, bufcount, dt, fill, ds, base=base)
+        torch.cuda.synchronize()
+        got_x, st = dx.cpu().numpy()[:n * xsz].tobytes(), int(ds.item())
+    assert st == exp_st and got_x == exp_x
+    # ---- get: convert + unpack; everything else in the user buffer survives
+    vals, gst = ora.getn(5, xt, exp_x, it)
+    exp_ub = ub.copy()
+    exp_ub[src.reshape(-1)] = np.ascontiguousarray(vals).view(np.uint8)
+    if where == "host":
+        out = ub.copy()
+        st = pncx.getn_flex(5, xt, np.frombuffer(exp_x, np.uint8).copy(), out, count, imap, bufcount, dt, base=base)
+    else:
+        du = torch.from_numpy(ub.copy()).cuda()
+        dx = torch.from_numpy(np.frombuffer(exp_x + b"\0" * 16, np.uint8).copy()).cuda()
+        ds = torch.zeros(1, dtype=torch.int32, device="cuda")
+        pncx.dev_getn_flex(5, xt, dx, du, count, imap, bufcount, dt, ds, base=base)
+        torch.cuda.synchronize()
+        out, st = du.cpu().numpy(), int(ds.item())
+    assert st == gst
+    assert out.tobytes() == exp_ub.tobytes()
+    return dt
+
+
+@pytest.mark.parametrize("tname,disp,blen,ext,bufcount,layout", TYPES)
+@pytest.mark.parametrize("xt,it", PAIRS)
+@pytest.mark.parametrize("where", ["host", "dev"])
+def test_flex_typemap(torch_cuda, tname, disp, blen, ext, bufcount, layout, xt, it, where):
+    dt = run_case(torch_cuda, where, xt, it, disp, blen, ext, bufcount, None, None,
+                  seed=zlib.crc32(f"{tname}/{xt}/{it}".encode()))
+    assert dt.inq()["layout"] == layout
+
+
+@pytest.mark.parametrize("where", ["host", "dev"])
+def test_flex_with_imap(torch_cuda, where):
+    # 12 packed elements (2 copies x 6) read through a transposing imap
+    run_case(torch_cuda, where, T.NC_FLOAT, T.ITYPE_DOUBLE, [7, 0, 11, 3], [2, 1, 2, 1], 14, 2, [3, 4], [1, 3], 7)
+    run_case(torch_cuda, where, T.NC_INT, T.ITYPE_INT, [0, 4, 8], [2, 2, 2], 12, 2, [4, 3], [1, 4], 8)
+
+
+@pytest.mark.parametrize("where", ["host", "dev"])
+def test_flex_large_table(torch_cuda, where):
+    # 2^16 irregular runs (binary-search layout) x 4 copies, ~1M elements
+    rng = np.random.default_rng(5)
+    nb = 1 << 16
+    blen = rng.integers(1, 8, nb)
+    gaps = rng.integers(0, 5, nb)
+    disp = np.concatenate([[0], np.cumsum(blen + gaps)[:-1]]).astype(np.int64)
+    ext = int(disp[-1] + blen[-1] + 3)
+    dt = run_case(torch_cuda, where, T.NC_INT, T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(), ext, 4,
+                  None, None, 9)
+    assert dt.inq()["layout"] == 2
+
+
+@pytest.mark.parametrize("where", ["host", "dev"])
+def test_flex_large_uniform(torch_cuda, where):
+    # vector(2^18 blocks of 3, stride 5) x 2 copies
+    nb = 1 << 18
+    disp = (np.arange(nb) * 5).tolist()
+    dt = run_case(torch_cuda, where, T.NC_DOUBLE, T.ITYPE_DOUBLE, disp, [3] * nb, 5 * nb + 1, 2, None, None, 10)
+    assert dt.inq()["layout"] == 1
+
+
+def test_flex_mpi_file_parity(tmp_path):
+    """The whole flexible file path with real MPI datatypes (contiguous,
+    (h)vector, (h)indexed, (h)indexed_block, struct, subarray C/Fortran,
+    resized, nested, dup, darray) x 4 conversions: derived-type put/iput and
+    get/iget equal MPI_Pack + contiguous put and contiguous get + MPI_Unpack."""
+    exe = os.path.join(ROOT, "tests", "mpi", "flex_check")
+    assert os.path.exists(exe), "tests/mpi/flex_check not built (run __graft_entry__.build())"
+    r = subprocess.run([exe, "file", str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    assert "file: 0 failure(s)" in r.stdout
+    assert r.stdout.count("ok file") == 4 * 14

@@ -1,0 +1,104 @@
+"""Throughput of the fused pack+convert kernels (derived buftypes, varm) against
+the contiguous kernel on the same element count.  Device-resident; HIP events
+around each launch; algorithmic bytes = n * (xsize + isize) (the gaps between
+runs are not counted).
+
+Workloads (NC_DOUBLE external <- double user buffer, put direction):
+  halo3d    interior 254^3 of a 256^3 local array (ghost cells dropped): a 3-D
+            subarray buftype, 64516 runs of 254 elements -> general table
+  vector2   every other element (MPI_Type_vector(n, 1, 2)) -> uniform runs
+  vector64  runs of 64 every 80 -> uniform runs
+  transpose varm with imap = Fortran order over a 512 x 512 x 128 request
+  contig    plain pncx_dev_putn on the same n (the roofline reference)
+
+    python tools/flex_bench.py [--reps 10]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    import torch
+    from pnetcdf_amd import nctypes as T
+    from pnetcdf_amd import pncx
+    lib = pncx.lib()
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    fb = np.frombuffer(T.fill_bytes(T.NC_DOUBLE) + b"\0" * 8, np.uint8).copy()
+    fp = ctypes.c_void_p(fb.ctypes.data)
+
+    def offs(v):
+        a = np.ascontiguousarray(np.asarray(v, np.int64))
+        return a, ctypes.c_void_p(a.ctypes.data)
+
+    def timeit(fn, n):
+        fn()
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.reps)]
+        for a, b in ev:
+            a.record()
+            fn()
+            b.record()
+        torch.cuda.synchronize()
+        ms = sorted(a.elapsed_time(b) for a, b in ev)[len(ev) // 2]
+        return ms, n * 16 / ms / 1e6
+
+    res = []
+    # halo3d: 256^3 local array, interior 254^3
+    L, I = 256, 254
+    ub = torch.empty(L ** 3 * 8, dtype=torch.uint8, device="cuda")
+    ub.view(torch.float64).normal_()
+    z, y = np.meshgrid(np.arange(I), np.arange(I), indexing="ij")
+    disp = (((z + 1) * L * L + (y + 1) * L + 1) * 8).reshape(-1)
+    dt = pncx.DType(T.ITYPE_DOUBLE, disp.tolist(), [I] * disp.size, L ** 3 * 8)
+    n = I ** 3
+    xb = torch.empty(n * 8, dtype=torch.uint8, device="cuda")
+    c, cp = offs([n])
+    res.append(("halo3d", dt.inq()["layout"], n) + timeit(
+        lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(xb.data_ptr()), ctypes.c_void_p(ub.data_ptr()),
+                                       1, cp, None, 1, dt.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n))
+    res.append(("contig", -1, n) + timeit(
+        lambda: lib.pncx_dev_putn(5, T.NC_DOUBLE, ctypes.c_void_p(xb.data_ptr()), ctypes.c_void_p(ub.data_ptr()), n,
+                                  T.ITYPE_DOUBLE, fp, ctypes.c_void_p(st.data_ptr()), sp), n))
+    # vector2 / vector64 over 2^27 elements
+    for name, blen, stride in (("vector2", 1, 2), ("vector64", 64, 80)):
+        nb = (1 << 27) // blen
+        span = nb * stride * 8
+        u2 = torch.empty(span, dtype=torch.uint8, device="cuda")
+        dtv = pncx.DType(T.ITYPE_DOUBLE, (np.arange(nb, dtype=np.int64) * stride * 8).tolist(), [blen] * nb, span)
+        n2 = nb * blen
+        x2 = torch.empty(n2 * 8, dtype=torch.uint8, device="cuda")
+        c2, cp2 = offs([n2])
+        res.append((name, dtv.inq()["layout"], n2) + timeit(
+            lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(x2.data_ptr()),
+                                           ctypes.c_void_p(u2.data_ptr()), 1, cp2, None, 1, dtv.handle, fp,
+                                           ctypes.c_void_p(st.data_ptr()), sp), n2))
+        del u2, x2
+    # transpose varm
+    cnt = [512, 512, 128]
+    imap = [1, 512, 512 * 512]
+    n3 = 512 * 512 * 128
+    u3 = torch.empty(n3 * 8, dtype=torch.uint8, device="cuda")
+    x3 = torch.empty(n3 * 8, dtype=torch.uint8, device="cuda")
+    c3, cp3 = offs(cnt)
+    m3, mp3 = offs(imap)
+    res.append(("transpose", -1, n3) + timeit(
+        lambda: lib.pncx_dev_putn_imap(5, T.NC_DOUBLE, ctypes.c_void_p(x3.data_ptr()), ctypes.c_void_p(u3.data_ptr()),
+                                       3, cp3, mp3, T.ITYPE_DOUBLE, fp, ctypes.c_void_p(st.data_ptr()), sp), n3))
+    for name, layout, n, ms, gbs in res:
+        print(json.dumps({"workload": name, "layout": layout, "n": n, "ms": round(ms, 4),
+                          "GB_per_s": round(gbs, 1), "frac_of_8TBs": round(gbs / 8000, 4)}))
+
+
+if __name__ == "__main__":
+    main()
