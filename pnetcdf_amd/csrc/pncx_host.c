@@ -734,7 +734,11 @@ struct pncx_dtype {
     long long  lo, hi;                /* byte bounds of one copy: [lo, hi)     */
     long long  len, stride, disp0;    /* layout 0/1                            */
     long long *pre, *disp;            /* host table (nblk each)                */
-    long long *dtab;                  /* device: pre[nblk] then disp[nblk]     */
+    long long *dtab;                  /* device: pieces of the runs (<= PNCX_TMAP_PIECE
+                                       * elements): pre[np + 1], disp[np], then
+                                       * cidx[nq + 1], the piece of element 64q */
+    long long  np, nq;                /* pieces, 64-element chunks             */
+    int        runmajor;              /* runs long enough for one wave each    */
 };
 
 int pncx_type_commit(int itype, pncx_offset nblocks, const pncx_offset *disp,
@@ -795,17 +799,50 @@ int pncx_type_commit(int itype, pncx_offset nblocks, const pncx_offset *disp,
     }
     free(len);
     if (t->layout == 2 && have_device()) {
-        /* the general table lives in HBM from now on: device calls stay async */
-        const size_t tb = sizeof(long long) * (size_t)k;
-        if (pncxrt_malloc((void **)&t->dtab, 2 * tb) != 0 ||
-            pncxrt_memcpy_h2d(t->dtab, t->pre, tb, NULL) != 0 ||
-            pncxrt_memcpy_h2d(t->dtab + k, t->disp, tb, NULL) != 0 ||
-            pncxrt_stream_sync(NULL) != 0) {
+        /* The general table lives in HBM from now on (device calls stay
+         * async), with runs split into pieces of at most PNCX_TMAP_PIECE
+         * elements: in packed order a wave then takes one piece when runs
+         * average >= 48 elements (k_tmap_runs), else lanes search the table. */
+        long long np = 0, p, e, nq, q;
+        int derr = 0;
+        long long *h;
+        for (i = 0; i < k; i++) {
+            const long long ln = (i + 1 < k ? t->pre[i + 1] : t->tn) - t->pre[i];
+            np += (ln + PNCX_TMAP_PIECE - 1) / PNCX_TMAP_PIECE;
+        }
+        nq = (t->tn + 63) / 64;
+        h = (long long *)malloc(sizeof(long long) * (size_t)(2 * np + 1 + nq + 1));
+        if (h == NULL) derr = NC_ENOMEM;
+        for (i = 0, p = 0; i < k && !derr; i++) {
+            const long long ln = (i + 1 < k ? t->pre[i + 1] : t->tn) - t->pre[i];
+            for (e = 0; e < ln; e += PNCX_TMAP_PIECE, p++) {
+                h[p] = t->pre[i] + e;
+                h[np + 1 + p] = t->disp[i] + e * isz;
+            }
+        }
+        if (!derr) {
+            long long *cidx = h + 2 * np + 1;
+            h[np] = t->tn;
+            for (q = 0, p = 0; q < nq; q++) {         /* piece holding element 64q */
+                while (p + 1 < np && h[p + 1] <= 64 * q) p++;
+                cidx[q] = p;
+            }
+            cidx[nq] = np - 1;
+            t->np = np;
+            t->nq = nq;
+            t->runmajor = t->tn >= 48 * k;
+            if (pncxrt_malloc((void **)&t->dtab, sizeof(long long) * (size_t)(2 * np + 1 + nq + 1)) != 0 ||
+                pncxrt_memcpy_h2d(t->dtab, h, sizeof(long long) * (size_t)(2 * np + 1 + nq + 1), NULL) != 0 ||
+                pncxrt_stream_sync(NULL) != 0)
+                derr = PNCX_EDEVICE;
+        }
+        free(h);
+        if (derr) {
             pncxrt_free(t->dtab);
             free(t->pre);
             free(t->disp);
             free(t);
-            return PNCX_EDEVICE;
+            return derr;
         }
     }
     *dtype = t;
@@ -863,27 +900,30 @@ static int flex_layout(int ndims, const pncx_offset *count, const pncx_offset *i
     long long span;
     *lo = *hi = 0;
     if (t == NULL || bufcount < 0) { *err = NC_EINVAL; return -1; }
+    int packed_order = 0;
     if (!imap_layout(ndims, count, imap, m, n, &span, err)) {
         if (*err != NC_NOERR) return -1;
         m->ndims = 1;                     /* packed order: offset = k */
         m->count[0] = *n;
         m->imap[0] = 1;
         m->max_count = *n;
+        packed_order = 1;
     }
     if (bufcount * t->tn != *n) { *err = NC_EIOMISMATCH; return -1; }   /* dtype_decode.c:690 */
     if (t->layout == 0 || (t->nblk == 1 && bufcount == 1)) {
         *lo = t->nblk ? t->disp0 : 0;
         return 0;
     }
-    m->tmode = t->layout;
+    m->tmode = t->layout == 2 && t->runmajor && packed_order ? 3 : t->layout;
     m->tn = t->tn;
     m->textent = t->extent;
     m->tlen = t->len;
     m->tstride = t->stride;
     m->tdisp0 = t->disp0;
-    m->tnblk = t->nblk;
+    m->tnblk = t->layout == 2 ? t->np : t->nblk;
     m->tpre = t->dtab;
-    m->tdisp = t->dtab ? t->dtab + t->nblk : NULL;
+    m->tdisp = t->dtab ? t->dtab + t->np + 1 : NULL;
+    m->tcidx = t->dtab ? t->dtab + 2 * t->np + 1 : NULL;
     {
         const long long last = (bufcount - 1) * t->extent;
         *lo = t->lo < last + t->lo ? t->lo : last + t->lo;
@@ -907,7 +947,7 @@ int pncx_dev_putn_flex(int cdf_ver, int xtype, void *dxbuf, const void *dbuf, in
         return pncx_dev_putn_imap(cdf_ver, xtype, dxbuf, (const char *)dbuf + lo, ndims, count, imap,
                                   bt->itype, fillp, dstatus, stream);
     if (n <= 0) return NC_NOERR;
-    if (!have_device() || (m.tmode == 2 && m.tpre == NULL)) return PNCX_EDEVICE;
+    if (!have_device() || (m.tmode >= 2 && m.tpre == NULL)) return PNCX_EDEVICE;
     return launch_imap_op(&op, dbuf, dxbuf, n, &m, 1, dstatus, stream);
 }
 
@@ -926,7 +966,7 @@ int pncx_dev_getn_flex(int cdf_ver, int xtype, const void *dxbuf, void *dbuf, in
         return pncx_dev_getn_imap(cdf_ver, xtype, dxbuf, (char *)dbuf + lo, ndims, count, imap,
                                   bt->itype, dstatus, stream);
     if (n <= 0) return NC_NOERR;
-    if (!have_device() || (m.tmode == 2 && m.tpre == NULL)) return PNCX_EDEVICE;
+    if (!have_device() || (m.tmode >= 2 && m.tpre == NULL)) return PNCX_EDEVICE;
     return launch_imap_op(&op, dxbuf, dbuf, n, &m, 0, dstatus, stream);
 }
 
@@ -952,7 +992,7 @@ static int host_flex(int dir, int cdf_ver, int xtype, void *xbuf, void *buf, int
                    ? pncx_putn_imap(cdf_ver, xtype, xbuf, (const char *)buf + lo, ndims, count, imap, bt->itype, fillp)
                    : pncx_getn_imap(cdf_ver, xtype, xbuf, (char *)buf + lo, ndims, count, imap, bt->itype);
     if (n <= 0) return NC_NOERR;
-    if (!have_device() || (m.tmode == 2 && m.tpre == NULL)) return PNCX_EDEVICE;
+    if (!have_device() || (m.tmode >= 2 && m.tpre == NULL)) return PNCX_EDEVICE;
     c = get_ctx();
     if (c == NULL) return PNCX_EDEVICE;
     xs = (size_t)pncx_xlen(xtype);

@@ -423,25 +423,34 @@ __device__ __forceinline__ int64_t imap_offset(IDX k, const pncxk_imap &m) {
     return off + (int64_t)k * m.imap[0];
 }
 
-// Byte offset of packed element j of a flattened derived buftype (the typemap
-// MPI_Pack walks, dtype_decode.c:628-694 + ncmpio_util.c:620-652): copy
-// c = j / tn, element r = j % tn inside it, found in block b by a binary search
-// over the block prefix (tmode 2) or by a divide (uniform blocks, tmode 1).
-template <int ES>
-__device__ __forceinline__ int64_t tmap_byte(int64_t j, const pncxk_imap &m) {
-    const int64_t c = j / m.tn;
-    const int64_t r = j - c * m.tn;
-    if (m.tmode == 1) {
-        const int64_t q = r / m.tlen;
-        return c * m.textent + m.tdisp0 + q * m.tstride + (r - q * m.tlen) * ES;
-    }
-    int64_t lo = 0, hi = m.tnblk - 1;
+// Derived buftype (the typemap MPI_Pack walks, dtype_decode.c:628-694 +
+// ncmpio_util.c:620-652): packed element j is element r = j % tn of copy
+// c = j / tn, in run b (pre[b] <= r < pre[b+1]) at byte c*extent + disp[b] +
+// (r - pre[b])*ES.
+
+// largest b in [lo, hi] with pre[b] <= r
+__device__ __forceinline__ int64_t run_search(const long long *pre, int64_t r, int64_t lo, int64_t hi) {
     while (lo < hi) {
         const int64_t mid = (lo + hi + 1) >> 1;
-        if (m.tpre[mid] <= r) lo = mid;
+        if (pre[mid] <= r) lo = mid;
         else hi = mid - 1;
     }
-    return c * m.textent + m.tdisp[lo] + (r - m.tpre[lo]) * ES;
+    return lo;
+}
+
+// any element (imap'ed order): uniform runs by division, tables by search
+template <int ES, typename IDX>
+__device__ __forceinline__ int64_t tmap_byte(int64_t j, const pncxk_imap &m) {
+    const IDX c = (IDX)j / (IDX)m.tn;
+    const IDX r = (IDX)j - c * (IDX)m.tn;
+    if (m.tmode == 1) {
+        const IDX q = r / (IDX)m.tlen;
+        return (int64_t)c * m.textent + m.tdisp0 + (int64_t)q * m.tstride + (int64_t)(r - q * (IDX)m.tlen) * ES;
+    }
+    // the 64-element index narrows the search to the blocks of r's chunk
+    const IDX q = r >> 6;
+    const int64_t b = run_search(m.tpre, (int64_t)r, m.tcidx[q], m.tcidx[q + 1]);
+    return (int64_t)c * m.textent + m.tdisp[b] + ((int64_t)r - m.tpre[b]) * ES;
 }
 
 // GATHER = true: src strided (user, put); false: dst strided (user, get)
@@ -450,36 +459,182 @@ __global__ __launch_bounds__(256) void k_imap(const uint8_t *src, uint8_t *dst, 
                                               typename Op::fill_t fill, int *status) {
     using SU = typename Op::SU;
     using DU = typename Op::DU;
+    constexpr int UES = GATHER ? Op::SS : Op::DS;      // user element size
     const int64_t stride = (int64_t)gridDim.x * 256;
     bool bad = false;
     for (int64_t k = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 + threadIdx.x; k < n; k += stride) {
-        const int64_t u = imap_offset<IDX>((IDX)k, m);          // user element offset
-        const uint8_t *ps;
-        uint8_t *pd;
-        if constexpr (GATHER) {
-            ps = src + (m.tmode ? tmap_byte<Op::SS>(u, m) : u * Op::SS);
-            pd = dst + k * Op::DS;
-        } else {
-            ps = src + k * Op::SS;
-            pd = dst + (m.tmode ? tmap_byte<Op::DS>(u, m) : u * Op::DS);
-        }
-        const SU s = ld_unaligned<SU>(ps);
+        const int64_t j = imap_offset<IDX>((IDX)k, m);          // user element index
+        const int64_t u = m.tmode ? tmap_byte<UES, IDX>(j, m) : j * UES;
+        const uint8_t *ps = GATHER ? src + u : src + k * Op::SS;
+        uint8_t *pd = GATHER ? dst + k * Op::DS : dst + u;
         DU old = 0;
         if constexpr (Op::PRESERVE) old = ld_unaligned<DU>(pd);
-        st_unaligned<DU>(pd, Op::one(s, old, fill, bad));
+        st_unaligned<DU>(pd, Op::one(ld_unaligned<SU>(ps), old, fill, bad));
     }
     publish_status(status, bad);
+}
+
+// Derived buftype in packed order with long runs (tmode 3): one wave per run
+// piece (pieces of at most PNCX_TMAP_PIECE elements, split at commit), lanes
+// along the piece -- both sides contiguous, no search.  c = copy, b = piece.
+template <class Op, bool GATHER>
+__global__ __launch_bounds__(256) void k_tmap_runs(const uint8_t *src, uint8_t *dst, int64_t n, pncxk_imap m,
+                                                   typename Op::fill_t fill, int *status) {
+    using SU = typename Op::SU;
+    using DU = typename Op::DU;
+    constexpr int UES = GATHER ? Op::SS : Op::DS;
+    const int lane = threadIdx.x & 63;
+    const int64_t total = n / m.tn * m.tnblk;            // pieces over all copies
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    bool bad = false;
+    for (int64_t g = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6); g < total; g += nw) {
+        const int64_t c = g / m.tnblk, b = g - c * m.tnblk;
+        const int64_t p0 = m.tpre[b], len = m.tpre[b + 1] - p0;
+        const int64_t ub = c * m.textent + m.tdisp[b];    // user byte offset of the piece
+        const int64_t kb = c * m.tn + p0;                   // packed element of the piece
+        for (int64_t e = lane; e < len; e += 64) {
+            const uint8_t *ps = GATHER ? src + ub + e * UES : src + (kb + e) * Op::SS;
+            uint8_t *pd = GATHER ? dst + (kb + e) * Op::DS : dst + ub + e * UES;
+            DU old = 0;
+            if constexpr (Op::PRESERVE) old = ld_unaligned<DU>(pd);
+            st_unaligned<DU>(pd, Op::one(ld_unaligned<SU>(ps), old, fill, bad));
+        }
+    }
+    publish_status(status, bad);
+}
+
+// ---------------------------------------------------------------------------
+// varm transpose: when the user buffer's fastest dimension U (smallest imap)
+// is not the packed order's fastest dimension P (the last), per-element
+// gathers touch one cache line per lane.  A 64 x 64 tile of (P, U) goes
+// through LDS instead: read coalesced along U in the user buffer, write
+// coalesced along P in the packed buffer (put); the reverse for get.  Other
+// dimensions index the tile grid.  The conversion runs on the packed side.
+// ---------------------------------------------------------------------------
+struct TransposeGeom {
+    int64_t cp, cu;          // count[P], count[U]
+    int64_t ip, iu;          // imap[P], imap[U] (user elements)
+    int64_t su;              // packed stride of U
+    int64_t tp, tu;          // tiles along P and U
+    int64_t ntiles;          // tp * tu * outer
+    int     nod;             // outer dims
+    int64_t ocount[PNCX_MAX_DIMS], ostride_p[PNCX_MAX_DIMS], ostride_u[PNCX_MAX_DIMS];
+};
+
+template <class Op, bool GATHER>
+__global__ __launch_bounds__(256) void k_imap_tile(const uint8_t *src, uint8_t *dst, TransposeGeom g,
+                                                   typename Op::fill_t fill, int *status) {
+    using SU = typename Op::SU;
+    using DU = typename Op::DU;
+    using TU = typename std::conditional<GATHER, SU, DU>::type;     // LDS holds user-side bits
+    constexpr int UES = GATHER ? Op::SS : Op::DS;
+    constexpr int PES = GATHER ? Op::DS : Op::SS;
+    __shared__ TU tile[64][65];
+    const int t = threadIdx.x, lo6 = t & 63, hi2 = t >> 6;
+    bool bad = false;
+    for (int64_t b = xcd_remap(blockIdx.x, gridDim.x); b < g.ntiles; b += gridDim.x) {
+        int64_t q = b;
+        const int64_t tu = q % g.tu;
+        q /= g.tu;
+        const int64_t tp = q % g.tp;
+        q /= g.tp;
+        int64_t pbase = 0, ubase = 0;
+        for (int d = g.nod - 1; d >= 0; d--) {          // outer dims, innermost last
+            const int64_t i = q % g.ocount[d];
+            q /= g.ocount[d];
+            pbase += i * g.ostride_p[d];
+            ubase += i * g.ostride_u[d];
+        }
+        const int64_t p0 = tp * 64, u0 = tu * 64;
+        const int np = (int)(g.cp - p0 < 64 ? g.cp - p0 : 64), nu = (int)(g.cu - u0 < 64 ? g.cu - u0 : 64);
+        if (GATHER) {
+            // user -> LDS, lanes along U
+            for (int r = hi2; r < np; r += 4)
+                if (lo6 < nu)
+                    tile[r][lo6] = ld_unaligned<TU>(src + (ubase + (p0 + r) * g.ip + (u0 + lo6) * g.iu) * UES);
+            __syncthreads();
+            // LDS -> convert -> packed, lanes along P
+            for (int c = hi2; c < nu; c += 4)
+                if (lo6 < np) {
+                    uint8_t *pd = dst + (pbase + (u0 + c) * g.su + p0 + lo6) * PES;
+                    DU old = 0;
+                    if constexpr (Op::PRESERVE) old = ld_unaligned<DU>(pd);
+                    st_unaligned<DU>(pd, Op::one(tile[lo6][c], old, fill, bad));
+                }
+        } else {
+            // packed -> convert -> LDS, lanes along P
+            for (int c = hi2; c < nu; c += 4)
+                if (lo6 < np)
+                    tile[lo6][c] = Op::one(ld_unaligned<SU>(src + (pbase + (u0 + c) * g.su + p0 + lo6) * PES),
+                                           DU(0), fill, bad);
+            __syncthreads();
+            // LDS -> user, lanes along U
+            for (int r = hi2; r < np; r += 4)
+                if (lo6 < nu) st_unaligned<TU>(dst + (ubase + (p0 + r) * g.ip + (u0 + lo6) * g.iu) * UES, tile[r][lo6]);
+        }
+        __syncthreads();
+    }
+    publish_status(status, bad);
+}
+
+// Pick the transpose kernel for a varm layout: P = last dim, U = the other
+// dim with the smallest imap; worth it when P is strided in the user buffer
+// and U is (nearly) contiguous there.
+inline bool transpose_geom(const pncxk_imap *m, TransposeGeom *g) {
+    const int nd = m->ndims, P = nd - 1;
+    int U = -1;
+    if (m->tmode != 0 || nd < 2) return false;
+    for (int d = 0; d < P; d++)
+        if (m->count[d] > 1 && (U < 0 || m->imap[d] < m->imap[U])) U = d;
+    if (U < 0 || m->count[P] < 16 || m->count[U] < 16) return false;
+    if (m->imap[P] <= 2 || m->imap[U] >= m->imap[P] || m->imap[U] > 2) return false;
+    int64_t pst[PNCX_MAX_DIMS];
+    int64_t s = 1;
+    for (int d = nd - 1; d >= 0; d--) { pst[d] = s; s *= m->count[d]; }
+    g->cp = m->count[P];
+    g->cu = m->count[U];
+    g->ip = m->imap[P];
+    g->iu = m->imap[U];
+    g->su = pst[U];
+    g->tp = (g->cp + 63) / 64;
+    g->tu = (g->cu + 63) / 64;
+    g->nod = 0;
+    int64_t outer = 1;
+    for (int d = 0; d < P; d++) {
+        if (d == U) continue;
+        g->ocount[g->nod] = m->count[d];
+        g->ostride_p[g->nod] = pst[d];
+        g->ostride_u[g->nod] = m->imap[d];
+        g->nod++;
+        outer *= m->count[d];
+    }
+    g->ntiles = g->tp * g->tu * outer;
+    return g->ntiles > 0;
 }
 
 template <class Op>
 int launch_imap(const pncxk_args *a, const pncxk_imap *m, int gather) {
     if (a->n <= 0) return 0;
-    const int grid = launch_grid(a->n, 4);
-    const bool small = a->n < (1LL << 32) && m->max_count < (1LL << 32);
     const uint8_t *src = (const uint8_t *)a->src;
     uint8_t *dst = (uint8_t *)a->dst;
     const typename Op::fill_t fill = (typename Op::fill_t)a->fill;
     hipStream_t st = (hipStream_t)a->stream;
+    TransposeGeom g;
+    if (m->tmode == 3) {
+        const int64_t pieces = a->n / m->tn * m->tnblk;
+        const unsigned grid = (unsigned)((pieces + 3) / 4 < MAX_BLOCKS ? (pieces + 3) / 4 : MAX_BLOCKS);
+        if (gather) hipLaunchKernelGGL((k_tmap_runs<Op, true>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, a->status);
+        else hipLaunchKernelGGL((k_tmap_runs<Op, false>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, a->status);
+        return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
+    }
+    if (transpose_geom(m, &g)) {
+        const unsigned grid = (unsigned)(g.ntiles < MAX_BLOCKS ? g.ntiles : MAX_BLOCKS);
+        if (gather) hipLaunchKernelGGL((k_imap_tile<Op, true>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, a->status);
+        else hipLaunchKernelGGL((k_imap_tile<Op, false>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, a->status);
+        return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
+    }
+    const int grid = launch_grid(a->n, 4);
+    const bool small = a->n < (1LL << 32) && m->max_count < (1LL << 32);
     if (gather) {
         if (small) hipLaunchKernelGGL((k_imap<Op, true, uint32_t>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, a->status);
         else hipLaunchKernelGGL((k_imap<Op, true, uint64_t>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, a->status);

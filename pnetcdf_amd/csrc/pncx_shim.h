@@ -59,6 +59,7 @@ typedef struct pncxk_batch_args {
 
 /* varm layout of the user buffer (create_imaptype.c semantics) */
 #define PNCX_MAX_DIMS 16
+#define PNCX_TMAP_PIECE 512
 typedef struct pncxk_imap {
     int       ndims;
     int       pad;
@@ -71,12 +72,15 @@ typedef struct pncxk_imap {
      * tmode 0: none, byte offset = j * element size
      *       1: uniform blocks of tlen elements, tstride bytes apart from tdisp0
      *       2: table, tnblk blocks, tpre[b] = first packed element of block b,
-     *          tdisp[b] = its byte displacement (device arrays) */
+     *          tdisp[b] = its byte displacement (device arrays; tpre[tnblk] = tn)
+     *       3: the same table, runs long enough for one wave per run (packed
+     *          order only; runs split into pieces of <= PNCX_TMAP_PIECE) */
     int       tmode;
     int       tpad;
     long long tn, textent, tlen, tstride, tdisp0, tnblk;
     const long long *tpre;
     const long long *tdisp;
+    const long long *tcidx;          /* tcidx[q]: the block holding element 64q (q <= ceil(tn/64)) */
 } pncxk_imap;
 
 typedef struct pncxk_opinfo {

@@ -152,6 +152,25 @@ def test_flex_large_table(torch_cuda, where):
 
 
 @pytest.mark.parametrize("where", ["host", "dev"])
+@pytest.mark.parametrize("imap", [False, True])
+def test_flex_long_runs(torch_cuda, where, imap):
+    """runs of 50..1500 elements: one wave per run piece (k_tmap_runs, runs
+    split into pieces of <= 512 at commit); through an imap the same piece
+    table is searched per element"""
+    rng = np.random.default_rng(11)
+    nb = 300
+    blen = rng.integers(50, 1500, nb)
+    gaps = rng.integers(0, 40, nb)
+    disp = np.concatenate([[5], 5 + np.cumsum(blen + gaps)[:-1]]).astype(np.int64)
+    ext = int(disp[-1] + blen[-1] + 7)
+    n = int(blen.sum()) * 3
+    count, im = ([3, n // 3], [1, 3]) if imap else (None, None)
+    dt = run_case(torch_cuda, where, T.NC_SHORT, T.ITYPE_FLOAT, disp.tolist(), blen.tolist(), ext, 3,
+                  count, im, 12)
+    assert dt.inq()["layout"] == 2
+
+
+@pytest.mark.parametrize("where", ["host", "dev"])
 def test_flex_large_uniform(torch_cuda, where):
     # vector(2^18 blocks of 3, stride 5) x 2 copies
     nb = 1 << 18

@@ -26,6 +26,12 @@ CASES = [
     ([5, 1, 9], [100, 0, 11]),        # count 1 dim with imap 0
     ([1000, 3], [3, 1000]),            # tall-skinny transpose
     ([6], [5]),                        # 1-D strided
+    # LDS-tiled transpose path (k_imap_tile): packed-fastest dim strided in the
+    # user buffer, another dim (nearly) contiguous there
+    ([37, 70], [1, 37]),              # 2-D Fortran order, partial edge tiles
+    ([65, 20, 130], [2, 130, 2600]),  # padded (imap 2) fastest user dim, outer dim between
+    ([3, 40, 50], [2000, 1, 40]),     # U in the middle, outer dim first
+    ([16, 16], [1, 16]),              # exactly one tile
 ]
 PAIRS = [(T.NC_INT, T.ITYPE_DOUBLE), (T.NC_SHORT, T.ITYPE_FLOAT), (T.NC_DOUBLE, T.ITYPE_DOUBLE),
          (T.NC_BYTE, T.ITYPE_INT), (T.NC_UINT64, T.ITYPE_SCHAR), (T.NC_FLOAT, T.ITYPE_FLOAT)]

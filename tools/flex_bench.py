@@ -84,6 +84,21 @@ def main():
                                            ctypes.c_void_p(u2.data_ptr()), 1, cp2, None, 1, dtv.handle, fp,
                                            ctypes.c_void_p(st.data_ptr()), sp), n2))
         del u2, x2
+    # short irregular runs (1..7 elements, gaps 0..4): per-element table search
+    rng = np.random.default_rng(5)
+    nb = 1 << 20
+    blen = rng.integers(1, 8, nb)
+    disp = np.concatenate([[0], np.cumsum(blen + rng.integers(0, 5, nb))[:-1]]).astype(np.int64) * 8
+    span = int(disp[-1]) + int(blen[-1]) * 8
+    u4 = torch.empty(span * 8, dtype=torch.uint8, device="cuda")
+    dts = pncx.DType(T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(), span)
+    n4 = int(blen.sum()) * 8
+    x4 = torch.empty(n4 * 8, dtype=torch.uint8, device="cuda")
+    c4, cp4 = offs([n4])
+    res.append(("short_runs", dts.inq()["layout"], n4) + timeit(
+        lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(x4.data_ptr()), ctypes.c_void_p(u4.data_ptr()),
+                                       1, cp4, None, 8, dts.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n4))
+    del u4, x4
     # transpose varm
     cnt = [512, 512, 128]
     imap = [1, 512, 512 * 512]
