@@ -276,6 +276,17 @@ int pncx_getn_flex(int cdf_ver, int xtype, const void *xbuf, void *buf, int ndim
                    const pncx_dtype *buftype);
 
 /* ------------------------------------------------------------------------ */
+/* Data comparison of ncmpidiff (src/utils/ncmpidiff/ncmpidiff_core.c:200-  */
+/* 236, CHECK_VAR_DIFF): the smallest index at which two HBM arrays of      */
+/* itype differ -- exactly (tolerance == 0), or (tolerance != 0) when the   */
+/* absolute difference exceeds tol_diff AND the ratio to the larger         */
+/* magnitude exceeds tol_ratio, with the reference's C arithmetic.          */
+/* *first = that index, or -1 when the arrays agree.  Synchronises stream.  */
+/* ------------------------------------------------------------------------ */
+int pncx_dev_first_diff(const void *da, const void *db, pncx_offset nelems, int itype, int tolerance,
+                        double tol_diff, double tol_ratio, pncx_offset *first, pncx_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
 /* Batched conversion: many independent requests in one launch per         */
 /* conversion class (replaces the per-request loop of                       */
 /* ncmpio_igetput_varm, ncmpio_i_getput.m4:300-303, and the per-request      */

@@ -290,6 +290,7 @@ typedef struct ctx_t {
     struct cls_t *cache_cls;
     size_t cache_soff, cache_moff;
     void  *ev;                /* completion event for the spin-wait */
+    unsigned long long *dfirst;   /* pncx_dev_first_diff result word */
 } ctx_t;
 
 static ctx_t g_ctx[MAX_DEV];
@@ -721,6 +722,34 @@ int pncx_getn_imap(int cdf_ver, int xtype, const void *xbuf, void *ibuf, int ndi
                    const pncx_offset *count, const pncx_offset *imap, int itype)
 {
     return host_imap(PNCX_GET, cdf_ver, xtype, (void *)xbuf, ibuf, ndims, count, imap, itype, NULL);
+}
+
+/* ------------------------------------------------------------------------ */
+/* ncmpidiff data comparison                                                  */
+/* ------------------------------------------------------------------------ */
+int pncx_dev_first_diff(const void *da, const void *db, pncx_offset nelems, int itype, int tolerance,
+                        double tol_diff, double tol_ratio, pncx_offset *first, pncx_stream_t stream)
+{
+    ctx_t *c;
+    unsigned long long h = ~0ULL;
+    int err;
+    if (first == NULL || pncx_ilen(itype) < 0) return first == NULL ? NC_EINVAL : NC_EBADTYPE;
+    *first = -1;
+    if (nelems <= 0) return NC_NOERR;
+    if (!have_device() || (c = get_ctx()) == NULL) return PNCX_EDEVICE;
+    pthread_mutex_lock(&c->lock);
+    if (c->dfirst == NULL && pncxrt_malloc((void **)&c->dfirst, sizeof(unsigned long long)) != 0) {
+        pthread_mutex_unlock(&c->lock);
+        return PNCX_EDEVICE;
+    }
+    err = pncxrt_memset(c->dfirst, 0xff, sizeof(unsigned long long), stream);
+    if (!err) err = pncxk_first_diff(da, db, nelems, itype, tolerance, tol_diff, tol_ratio, c->dfirst, stream);
+    if (!err) err = pncxrt_memcpy_d2h(&h, c->dfirst, sizeof h, stream);
+    if (!err) err = pncxrt_stream_sync(stream);
+    pthread_mutex_unlock(&c->lock);
+    if (err) return err < 0 ? err : PNCX_EDEVICE;
+    *first = h == ~0ULL ? -1 : (pncx_offset)h;
+    return NC_NOERR;
 }
 
 /* ------------------------------------------------------------------------ */

@@ -107,6 +107,10 @@ int pncxk_launch_imap(int kind, int a, int b, int c, const pncxk_args *args, con
 int pncxk_opinfo_get(int kind, int a, int b, int c, pncxk_opinfo *o);
 /* replicate an xsize-byte external value over nelems elements (device) */
 int pncxk_fill(void *dst, long long nelems, int xsize, const void *xvalue, void *stream);
+/* smallest index where a and b (n elements of itype) differ, exactly or
+ * beyond both tolerances (ncmpidiff); atomicMin into *first (device) */
+int pncxk_first_diff(const void *a, const void *b, long long n, int itype, int tol, double td, double tr,
+                     unsigned long long *first, void *stream);
 /* fill args->dmap (nblocks ints) from the device descriptors */
 int pncxk_batch_map(const pncxk_batch_args *args);
 

@@ -44,3 +44,6 @@ int pncxk_launch_imap(int k, int a, int b, int c, const pncxk_args *x, const pnc
 int pncxk_opinfo_get(int k, int a, int b, int c, pncxk_opinfo *o) { (void)k; (void)a; (void)b; (void)c; (void)o; return NODEV; }
 int pncxk_fill(void *d, long long n, int x, const void *v, void *s) { (void)d; (void)n; (void)x; (void)v; (void)s; return NODEV; }
 int pncxk_batch_map(const pncxk_batch_args *x) { (void)x; return NODEV; }
+int pncxk_first_diff(const void *a, const void *b, long long n, int t, int tol, double td, double tr,
+                     unsigned long long *f, void *s)
+{ (void)a; (void)b; (void)n; (void)t; (void)tol; (void)td; (void)tr; (void)f; (void)s; return NODEV; }
