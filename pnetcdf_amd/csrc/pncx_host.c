@@ -1223,7 +1223,8 @@ static int batch_plan(plan_t *p)
             sg->dst = it[k].dst;
             sg->n = it[k].n;
             sg->head = h;
-            sg->nvec = (it[k].n - h) / oi.vec;           /* full block tiles */
+            /* full block tiles (the mix kernel's tile is PNCXK_MIX_LANES x 16 B) */
+            sg->nvec = (it[k].n - h) / (mix ? PNCXK_MIX_LANES * 16 / it[k].op.a : oi.vec);
             sg->block0 = c->nblocks;
             sg->fill = it[k].op.fill;
             sg->status = (int *)(intptr_t)it[k].idx;     /* caller's index; pointer set at run time */

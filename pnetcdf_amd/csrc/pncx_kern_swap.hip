@@ -131,47 +131,70 @@ extern "C" int pncxk_batch_get(int xtype, int itype, const pncxk_batch_args *a);
 extern "C" int pncxk_batch_put(int xtype, int itype, int preserve, const pncxk_batch_args *a);
 extern "C" int pncxk_opinfo_getput(int kind, int xtype, int itype, int preserve, pncxk_opinfo *o);
 
+constexpr int MIX_LANES = PNCXK_MIX_LANES;
+
 // One launch for all same-type segments of a batch (C4: NC_SHORT and
-// NC_FLOAT iputs): the block's segment says its element size; the tile body
-// is the same as for the single-size classes.
-template <bool NT>
-__global__ __launch_bounds__(256) void k_batch_swapmix(const pncxk_seg *segs, int nseg, long long uniform,
-                                                       const int *map, pncxk_groups grp, int sval) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[16];
+// NC_FLOAT iputs): the block's segment says its element size.  A block is
+// MIX_LANES lanes x 16 B (one nontemporal vector each, no loop).  On the C4
+// shape (1.5 GiB moved over 512 buffers) block size and order change the rate
+// by less than the spread between processes: 256/512/1024 lanes all land at
+// 77-87 % of HBM peak depending on where the buffers were placed, against
+// 81-83 % for one contiguous buffer of the same bytes (tools/batch_sweep.hip,
+// profiles/r01_batch_sweep*.txt).  1024 lanes = 4x fewer blocks to schedule.
+__device__ __forceinline__ u32x4 swap16(u32x4 v, int es) {
+    u32x4 r = v;
+    if (es == 2) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) r[k] = ((v[k] & 0x00ff00ffu) << 8) | ((v[k] >> 8) & 0x00ff00ffu);
+    } else if (es == 4) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) r[k] = __builtin_bswap32(v[k]);
+    } else if (es == 8) {
+        r[0] = __builtin_bswap32(v[1]); r[1] = __builtin_bswap32(v[0]);
+        r[2] = __builtin_bswap32(v[3]); r[3] = __builtin_bswap32(v[2]);
+    }
+    return r;                              // es == 1: copy
+}
+
+template <int ES>
+__device__ __forceinline__ void mix_scalar(const uint8_t *src, uint8_t *dst, int64_t e0, int64_t e1) {
+    using Op = SwapOp<ES>;
+    bool bad = false;
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += MIX_LANES) scalar_elem<Op>(src, dst, e, 0, bad);
+}
+
+__global__ __launch_bounds__(MIX_LANES) void k_batch_swapmix(const pncxk_seg *segs, int nseg, long long uniform,
+                                                             const int *map, pncxk_groups grp) {
     const long long b = blockIdx.x;
     const int s = batch_segment(b, uniform, map, grp, segs, nseg);
     const pncxk_seg sg = segs[s];
     const uint8_t *src = (const uint8_t *)sg.src;
     uint8_t *dst = (uint8_t *)sg.dst;
+    const int es = sg.aux;
     const int64_t rel = b - sg.block0;
-    bool bad = false;
-    switch (sg.aux) {
-#define PNCX_MIX(ES)                                                                               \
-        case ES: {                                                                                 \
-            using Op = SwapOp<ES>;                                                                 \
-            using S = Shape<Op>;                                                                   \
-            if (rel == 0) {                                                                        \
-                for (int64_t e = threadIdx.x; e < sg.head; e += 256) scalar_elem<Op>(src, dst, e, 0, bad); \
-                scalar_range<Op>(src, dst, sg.head + sg.nvec * S::TILE, sg.n, 0, bad);            \
-            }                                                                                      \
-            if (rel < sg.nvec)                                                                     \
-                tile_body<Op, NT>(src + (sg.head + rel * (int64_t)S::TILE) * ES,                   \
-                                  dst + (sg.head + rel * (int64_t)S::TILE) * ES, 0, bad, lds);     \
-            break;                                                                                 \
-        }
-        PNCX_MIX(1) PNCX_MIX(2) PNCX_MIX(4) PNCX_MIX(8)
-#undef PNCX_MIX
-        default: break;
+    if (rel < sg.nvec) {
+        const int64_t off = sg.head * es + (rel * MIX_LANES + threadIdx.x) * 16;
+        st16<true>(dst + off, swap16(ld16<true>(src + off), es));
     }
-    (void)sval;    // swaps never produce NC_ERANGE
+    if (rel == 0) {                        // scalar head and remainder (one lane per element)
+        const int64_t tail0 = sg.head + sg.nvec * (int64_t)(MIX_LANES * 16 / es);
+        switch (es) {
+            case 1: mix_scalar<1>(src, dst, 0, sg.head); mix_scalar<1>(src, dst, tail0, sg.n); break;
+            case 2: mix_scalar<2>(src, dst, 0, sg.head); mix_scalar<2>(src, dst, tail0, sg.n); break;
+            case 4: mix_scalar<4>(src, dst, 0, sg.head); mix_scalar<4>(src, dst, tail0, sg.n); break;
+            case 8: mix_scalar<8>(src, dst, 0, sg.head); mix_scalar<8>(src, dst, tail0, sg.n); break;
+            default: break;
+        }
+    }
+    // swaps never produce NC_ERANGE: no status
 }
 
 extern "C" int pncxk_batch(int kind, int a, int b, int c, const pncxk_batch_args *args) {
     if (kind == PNCXK_SWAPMIX) {
         if (args->nblocks <= 0) return 0;
-        hipLaunchKernelGGL((k_batch_swapmix<true>), dim3((unsigned)args->nblocks), dim3(256), 0,
+        hipLaunchKernelGGL(k_batch_swapmix, dim3((unsigned)args->nblocks), dim3(MIX_LANES), 0,
                            (hipStream_t)args->stream, args->dsegs, args->nseg, args->uniform, args->dmap,
-                           args->grp, args->sval);
+                           args->grp);
         return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
     }
     if (kind == PNCXK_SWAP) {

@@ -95,6 +95,7 @@ typedef struct pncxk_opinfo {
 #define PNCXK_GET  1  /* a = xtype, b = itype  */
 #define PNCXK_PUT  2  /* a = xtype, b = itype, c = preserve */
 #define PNCXK_SWAPMIX 3  /* batch only: same-type swaps/copies of any of 1/2/4/8 bytes */
+#define PNCXK_MIX_LANES 1024  /* lanes (x 16 B) per block tile of the SWAPMIX kernel */
 
 /* ---- kernel launchers (HIP TUs) ---- */
 int pncxk_swap(int esize, const pncxk_args *a);          /* esize 1,2,4,8 */

@@ -153,9 +153,8 @@ int main(int argc, char **argv) {
 
 #define ONE2(U, NT, BS, XM) { const int64_t g = (nvec + (int64_t)BS * U - 1) / ((int64_t)BS * U); \
       add(std::string("one2 U") + #U + " nt" + #NT + " bs" + #BS + " xcd" + #XM, 2, [=] { hipLaunchKernelGGL((k_one2<U, NT, BS, XM>), dim3(g), dim3(BS), 0, 0, p, nvec); }); }
-    ONE2(1, true, 256, true) ONE2(1, true, 128, true) ONE2(1, true, 64, true) ONE2(1, true, 512, true)
-    ONE2(1, true, 1024, true) ONE2(2, true, 256, true) ONE2(2, true, 128, true) ONE2(2, true, 64, true)
-    ONE2(4, true, 64, true) ONE2(1, false, 64, true) ONE2(1, false, 128, true)
+    ONE2(1, true, 256, true) ONE2(1, true, 256, false) ONE2(1, true, 512, true) ONE2(1, true, 512, false)
+    ONE2(1, true, 1024, true) ONE2(1, true, 1024, false) ONE2(2, true, 1024, false) ONE2(2, true, 512, false)
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
