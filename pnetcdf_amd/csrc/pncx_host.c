@@ -768,7 +768,18 @@ struct pncx_dtype {
                                        * cidx[nq + 1], the piece of element 64q */
     long long  np, nq;                /* pieces, 64-element chunks             */
     int        runmajor;              /* runs long enough for one wave each    */
+    unsigned  *doff;                  /* device: byte offset - lo of each element
+                                       * of a copy (short-run tables, tmode 4) */
 };
+
+/* Largest typemap (elements per copy) that gets a per-element offset map:
+ * 4 B of HBM per element, read coalesced, instead of a table search per
+ * element.  PNCX_TOFF_MAX_ELEMS overrides (0 disables; read at commit). */
+static long long toff_max_elems(void)
+{
+    const char *e = getenv("PNCX_TOFF_MAX_ELEMS");
+    return e ? atoll(e) : (1LL << 26);
+}
 
 int pncx_type_commit(int itype, pncx_offset nblocks, const pncx_offset *disp,
                      const pncx_offset *blocklen, pncx_offset extent, pncx_dtype **dtype)
@@ -866,7 +877,22 @@ int pncx_type_commit(int itype, pncx_offset nblocks, const pncx_offset *disp,
                 derr = PNCX_EDEVICE;
         }
         free(h);
+        if (!derr && !t->runmajor && t->tn <= toff_max_elems() && t->hi - t->lo <= 0xffffffffLL) {
+            /* short runs: per-element map (offsets from lo fit 32 bits) */
+            unsigned *o = (unsigned *)malloc(sizeof(unsigned) * (size_t)t->tn);
+            if (o == NULL) derr = NC_ENOMEM;
+            for (i = 0; i < k && !derr; i++) {
+                const long long ln = (i + 1 < k ? t->pre[i + 1] : t->tn) - t->pre[i];
+                for (e = 0; e < ln; e++) o[t->pre[i] + e] = (unsigned)(t->disp[i] - t->lo + e * isz);
+            }
+            if (!derr && (pncxrt_malloc((void **)&t->doff, sizeof(unsigned) * (size_t)t->tn) != 0 ||
+                          pncxrt_memcpy_h2d(t->doff, o, sizeof(unsigned) * (size_t)t->tn, NULL) != 0 ||
+                          pncxrt_stream_sync(NULL) != 0))
+                derr = PNCX_EDEVICE;
+            free(o);
+        }
         if (derr) {
+            pncxrt_free(t->doff);
             pncxrt_free(t->dtab);
             free(t->pre);
             free(t->disp);
@@ -889,9 +915,10 @@ int pncx_type_free(pncx_dtype *t)
 {
     if (t == NULL) return NC_EINVAL;
     if (__atomic_sub_fetch(&t->refs, 1, __ATOMIC_ACQ_REL) > 0) return NC_NOERR;
-    if (t->dtab) {
+    if (t->dtab || t->doff) {
         pncxrt_stream_sync(NULL);
         pncxrt_free(t->dtab);
+        pncxrt_free(t->doff);
     }
     free(t->pre);
     free(t->disp);
@@ -943,7 +970,9 @@ static int flex_layout(int ndims, const pncx_offset *count, const pncx_offset *i
         *lo = t->nblk ? t->disp0 : 0;
         return 0;
     }
-    m->tmode = t->layout == 2 && t->runmajor && packed_order ? 3 : t->layout;
+    m->tmode = t->layout == 2 && t->runmajor && packed_order ? 3 : t->layout == 2 && t->doff ? 4 : t->layout;
+    m->toff = t->doff;
+    m->tlo = t->lo;
     m->tn = t->tn;
     m->textent = t->extent;
     m->tlen = t->len;

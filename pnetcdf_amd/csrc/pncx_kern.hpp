@@ -443,6 +443,7 @@ template <int ES, typename IDX>
 __device__ __forceinline__ int64_t tmap_byte(int64_t j, const pncxk_imap &m) {
     const IDX c = (IDX)j / (IDX)m.tn;
     const IDX r = (IDX)j - c * (IDX)m.tn;
+    if (m.tmode == 4) return (int64_t)c * m.textent + m.tlo + (int64_t)m.toff[r];
     if (m.tmode == 1) {
         const IDX q = r / (IDX)m.tlen;
         return (int64_t)c * m.textent + m.tdisp0 + (int64_t)q * m.tstride + (int64_t)(r - q * (IDX)m.tlen) * ES;
@@ -453,6 +454,9 @@ __device__ __forceinline__ int64_t tmap_byte(int64_t j, const pncxk_imap &m) {
     return (int64_t)c * m.textent + m.tdisp[b] + ((int64_t)r - m.tpre[b]) * ES;
 }
 
+// elements per lane in flight in the run-major typemap kernel
+constexpr int IMAP_U = 4;
+
 // GATHER = true: src strided (user, put); false: dst strided (user, get)
 template <class Op, bool GATHER, typename IDX>
 __global__ __launch_bounds__(256) void k_imap(const uint8_t *src, uint8_t *dst, int64_t n, pncxk_imap m,
@@ -462,6 +466,8 @@ __global__ __launch_bounds__(256) void k_imap(const uint8_t *src, uint8_t *dst, 
     constexpr int UES = GATHER ? Op::SS : Op::DS;      // user element size
     const int64_t stride = (int64_t)gridDim.x * 256;
     bool bad = false;
+    // (unrolling this loop with the loads first measured slower on the
+    // vector64 / short-run cases, unlike k_tmap_runs below)
     for (int64_t k = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 + threadIdx.x; k < n; k += stride) {
         const int64_t j = imap_offset<IDX>((IDX)k, m);          // user element index
         const int64_t u = m.tmode ? tmap_byte<UES, IDX>(j, m) : j * UES;
@@ -492,12 +498,26 @@ __global__ __launch_bounds__(256) void k_tmap_runs(const uint8_t *src, uint8_t *
         const int64_t p0 = m.tpre[b], len = m.tpre[b + 1] - p0;
         const int64_t ub = c * m.textent + m.tdisp[b];    // user byte offset of the piece
         const int64_t kb = c * m.tn + p0;                   // packed element of the piece
-        for (int64_t e = lane; e < len; e += 64) {
-            const uint8_t *ps = GATHER ? src + ub + e * UES : src + (kb + e) * Op::SS;
-            uint8_t *pd = GATHER ? dst + (kb + e) * Op::DS : dst + ub + e * UES;
-            DU old = 0;
-            if constexpr (Op::PRESERVE) old = ld_unaligned<DU>(pd);
-            st_unaligned<DU>(pd, Op::one(ld_unaligned<SU>(ps), old, fill, bad));
+        for (int64_t e0 = lane; e0 < len; e0 += 64 * IMAP_U) {     // loads first, then stores
+            SU sv[IMAP_U];
+            DU old[IMAP_U];
+#pragma unroll
+            for (int i = 0; i < IMAP_U; i++) {
+                const int64_t e = e0 + 64 * i;
+                if (e < len) {
+                    sv[i] = ld_unaligned<SU>(GATHER ? src + ub + e * UES : src + (kb + e) * Op::SS);
+                    old[i] = 0;
+                    if constexpr (Op::PRESERVE)
+                        old[i] = ld_unaligned<DU>(GATHER ? dst + (kb + e) * Op::DS : dst + ub + e * UES);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < IMAP_U; i++) {
+                const int64_t e = e0 + 64 * i;
+                if (e < len)
+                    st_unaligned<DU>(GATHER ? dst + (kb + e) * Op::DS : dst + ub + e * UES,
+                                     Op::one(sv[i], old[i], fill, bad));
+            }
         }
     }
     publish_status(status, bad);

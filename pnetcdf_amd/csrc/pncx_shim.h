@@ -74,13 +74,18 @@ typedef struct pncxk_imap {
      *       2: table, tnblk blocks, tpre[b] = first packed element of block b,
      *          tdisp[b] = its byte displacement (device arrays; tpre[tnblk] = tn)
      *       3: the same table, runs long enough for one wave per run (packed
-     *          order only; runs split into pieces of <= PNCX_TMAP_PIECE) */
+     *          order only; runs split into pieces of <= PNCX_TMAP_PIECE)
+     *       4: the same table, short runs: per-element byte map toff */
     int       tmode;
     int       tpad;
     long long tn, textent, tlen, tstride, tdisp0, tnblk;
     const long long *tpre;
     const long long *tdisp;
     const long long *tcidx;          /* tcidx[q]: the block holding element 64q (q <= ceil(tn/64)) */
+    /* tmode 4: short-run table with a per-element map: element r of a copy
+     * is at byte tlo + toff[r] (device array of tn, built at commit) */
+    const unsigned  *toff;
+    long long        tlo;
 } pncxk_imap;
 
 typedef struct pncxk_opinfo {

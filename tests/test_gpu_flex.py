@@ -152,6 +152,27 @@ def test_flex_large_table(torch_cuda, where):
 
 
 @pytest.mark.parametrize("where", ["host", "dev"])
+def test_flex_table_search_path(torch_cuda, where, monkeypatch):
+    """short-run tables normally get a per-element offset map at commit
+    (tmode 4); with the map disabled the same cases take the chunk-indexed
+    table search (tmode 2)"""
+    monkeypatch.setenv("PNCX_TOFF_MAX_ELEMS", "0")
+    for tname, disp, blen, ext, bufcount, layout in TYPES:
+        if layout == 2:
+            dt = run_case(torch_cuda, where, T.NC_SHORT, T.ITYPE_INT, disp, blen, ext, bufcount, None, None,
+                          seed=zlib.crc32(tname.encode()))
+            assert dt.inq()["layout"] == 2
+    run_case(torch_cuda, where, T.NC_FLOAT, T.ITYPE_DOUBLE, [7, 0, 11, 3], [2, 1, 2, 1], 14, 2, [3, 4], [1, 3], 7)
+    rng = np.random.default_rng(6)
+    nb = 1 << 14
+    blen = rng.integers(1, 8, nb)
+    gaps = rng.integers(0, 5, nb)
+    disp = np.concatenate([[0], np.cumsum(blen + gaps)[:-1]]).astype(np.int64)
+    run_case(torch_cuda, where, T.NC_INT, T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(), int(disp[-1] + blen[-1] + 3),
+             3, None, None, 13)
+
+
+@pytest.mark.parametrize("where", ["host", "dev"])
 @pytest.mark.parametrize("imap", [False, True])
 def test_flex_long_runs(torch_cuda, where, imap):
     """runs of 50..1500 elements: one wave per run piece (k_tmap_runs, runs

@@ -98,6 +98,12 @@ def main():
     res.append(("short_runs", dts.inq()["layout"], n4) + timeit(
         lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(x4.data_ptr()), ctypes.c_void_p(u4.data_ptr()),
                                        1, cp4, None, 8, dts.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n4))
+    os.environ["PNCX_TOFF_MAX_ELEMS"] = "0"              # the same typemap without the offset map
+    dts2 = pncx.DType(T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(), span)
+    del os.environ["PNCX_TOFF_MAX_ELEMS"]
+    res.append(("short_runs_search", dts2.inq()["layout"], n4) + timeit(
+        lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(x4.data_ptr()), ctypes.c_void_p(u4.data_ptr()),
+                                       1, cp4, None, 8, dts2.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n4))
     del u4, x4
     # transpose varm
     cnt = [512, 512, 128]
@@ -110,6 +116,19 @@ def main():
     res.append(("transpose", -1, n3) + timeit(
         lambda: lib.pncx_dev_putn_imap(5, T.NC_DOUBLE, ctypes.c_void_p(x3.data_ptr()), ctypes.c_void_p(u3.data_ptr()),
                                        3, cp3, mp3, T.ITYPE_DOUBLE, fp, ctypes.c_void_p(st.data_ptr()), sp), n3))
+    # the same transpose with non-power-of-two extents (strides off the channel interleave)
+    for cnt in ([500, 500, 120], [512, 512, 120], [500, 512, 128]):
+        imap = [1, cnt[0], cnt[0] * cnt[1]]
+        n5 = cnt[0] * cnt[1] * cnt[2]
+        u5 = torch.empty(n5 * 8, dtype=torch.uint8, device="cuda")
+        x5 = torch.empty(n5 * 8, dtype=torch.uint8, device="cuda")
+        c5, cp5 = offs(cnt)
+        m5, mp5 = offs(imap)
+        res.append(("transpose_%dx%dx%d" % tuple(cnt), -1, n5) + timeit(
+            lambda: lib.pncx_dev_putn_imap(5, T.NC_DOUBLE, ctypes.c_void_p(x5.data_ptr()),
+                                           ctypes.c_void_p(u5.data_ptr()), 3, cp5, mp5, T.ITYPE_DOUBLE, fp,
+                                           ctypes.c_void_p(st.data_ptr()), sp), n5))
+        del u5, x5
     for name, layout, n, ms, gbs in res:
         print(json.dumps({"workload": name, "layout": layout, "n": n, "ms": round(ms, 4),
                           "GB_per_s": round(gbs, 1), "frac_of_8TBs": round(gbs / 8000, 4)}))
