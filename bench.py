@@ -247,6 +247,10 @@ def main():
     for _ in range(args.warmup):
         launch()
     torch.cuda.synchronize()
+    if args.workload == "c4":
+        # the batch call also copies the statuses back and waits: its kernel
+        # time comes from HIP events the library records around the launch
+        lib.pncx_dev_batch_timing(1)
 
     # ---------------------------------------------------------- timed region
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -262,6 +266,12 @@ def main():
     group.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    call_ms = None
+    if args.workload == "c4":
+        tot, calls = ctypes.c_double(), ctypes.c_longlong()
+        assert lib.pncx_dev_batch_kernel_ms(ctypes.byref(tot), ctypes.byref(calls)) == 0 and calls.value == args.steps
+        call_ms, kern_ms = kern_ms, tot.value / calls.value
+        lib.pncx_dev_batch_timing(0)
     elapsed, kern_ms = group.max([elapsed, kern_ms])         # max over ranks
 
     gather = None
@@ -298,6 +308,7 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "kernel_ms_avg": round(kern_ms, 4),
+                         **({"call_ms_avg": round(call_ms, 4)} if call_ms is not None else {}),
                          "algorithmic_bytes_per_launch": bytes_per_elem * elems},
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,

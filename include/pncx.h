@@ -309,6 +309,15 @@ typedef struct pncx_seg {
 int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out,
                    pncx_stream_t stream);
 
+/* Measurement aid (no reference counterpart): with timing enabled, every
+ * pncx_dev_batch call on the current device records HIP events on its stream
+ * around its batch kernels only (not the descriptor upload, the status copy
+ * or the wait).  pncx_dev_batch_kernel_ms returns the summed kernel time and
+ * the number of calls timed since pncx_dev_batch_timing(1) (which resets
+ * both). */
+int pncx_dev_batch_timing(int enable);
+int pncx_dev_batch_kernel_ms(double *total_ms, long long *calls);
+
 /* Host buffers (staged through HBM). */
 int pncx_batch(const pncx_seg *segs, int nseg, int *status_out);
 

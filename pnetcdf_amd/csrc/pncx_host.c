@@ -290,6 +290,10 @@ typedef struct ctx_t {
     struct cls_t *cache_cls;
     size_t cache_soff, cache_moff;
     void  *ev;                /* completion event for the spin-wait */
+    int    timing;            /* pncx_dev_batch_timing: events around the batch kernels */
+    void  *tev0, *tev1;
+    double tms;               /* summed kernel time of the timed batch calls */
+    long long tcalls;         /* ... and their number                         */
     unsigned long long *dfirst;   /* pncx_dev_first_diff result word */
 } ctx_t;
 
@@ -1294,11 +1298,22 @@ static int batch_plan(plan_t *p)
 /* scratch layout (device and pinned mirror): [statuses | descriptors | maps].
  * ONE upload zeroes the statuses and installs the descriptors; then the
  * unbatched items and the class kernels run; one copy brings the statuses back. */
+/* pncx_dev_batch_timing: add the kernel time of the call that just completed */
+static void batch_time(ctx_t *c)
+{
+    float ms = 0.0f;
+    if (pncxrt_event_elapsed_ms(&ms, c->tev0, c->tev1) == 0) {
+        c->tms += ms;
+        c->tcalls++;
+    }
+}
+
 /* launch the class kernels of a plan whose descriptors are on the device */
 static int launch_classes(const cls_t *cls, int ncls, uint8_t *dbase, size_t soff, size_t moff, int sval,
-                          int build_maps, void *stream)
+                          int build_maps, void *stream, ctx_t *tc)
 {
     int k, err = 0;
+    if (tc != NULL && tc->timing) err = pncxrt_event_record(tc->tev0, stream);
     pncxk_seg *dseg = (pncxk_seg *)(dbase + soff);
     int *dmap = (int *)(dbase + moff);
     for (k = 0; k < ncls && !err; k++) {
@@ -1315,11 +1330,12 @@ static int launch_classes(const cls_t *cls, int ncls, uint8_t *dbase, size_t sof
         if (ba.dmap != NULL && build_maps) err = pncxk_batch_map(&ba);
         if (!err) err = pncxk_batch(c->op.kind, c->op.a, c->op.b, c->op.c, &ba);
     }
+    if (!err && tc != NULL && tc->timing) err = pncxrt_event_record(tc->tev1, stream);
     return err;
 }
 
 static int batch_run(plan_t *p, int nseg, uint8_t *dbase, uint8_t *hbase, size_t soff, size_t moff,
-                     int sval, void *stream)
+                     int sval, void *stream, ctx_t *tc)
 {
     int k, err = 0;
     int *dstat = (int *)dbase;
@@ -1339,7 +1355,7 @@ static int batch_run(plan_t *p, int nseg, uint8_t *dbase, uint8_t *hbase, size_t
         if (b->op.kind == PNCXK_SWAP && b->op.a == 1 && b->src == b->dst) continue;
         err = launch_op(&b->op, b->src, b->dst, b->n, dstat + b->idx, stream);
     }
-    if (!err) err = launch_classes(p->cls, p->ncls, dbase, soff, moff, sval, 1, stream);
+    if (!err) err = launch_classes(p->cls, p->ncls, dbase, soff, moff, sval, 1, stream, tc);
     return err;
 }
 
@@ -1385,9 +1401,10 @@ int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_
     if (c->cache_valid && c->cache_nseg == nseg &&
         memcmp(c->cache_segs, segs, sizeof(pncx_seg) * (size_t)nseg) == 0) {
         err = launch_classes(c->cache_cls, c->cache_ncls, (uint8_t *)c->dscratch, c->cache_soff, c->cache_moff,
-                             sval, 0, stream);
+                             sval, 0, stream, c);
         if (!err) err = pncxrt_memcpy_d2h(c->hscratch, c->dscratch, sizeof(int) * (size_t)nseg, stream);
         if (!err) err = spin_wait(c, stream);
+        if (!err && c->timing) batch_time(c);
         if (!err)
             for (i = 0; i < nseg; i++) hstat[i] = ((int *)c->hscratch)[i] == sval ? NC_ERANGE : NC_NOERR;
         pthread_mutex_unlock(&c->lock);
@@ -1419,10 +1436,12 @@ int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_
         const size_t moff = soff + ALIGN16(sizeof(pncxk_seg) * (size_t)(plan.nsegd + 1));
         err = ensure_scratch(c, moff + sizeof(int) * (size_t)plan.map_ints + 16);
         if (!err)
-            err = batch_run(&plan, nseg, (uint8_t *)c->dscratch, (uint8_t *)c->hscratch, soff, moff, sval, stream);
+            err = batch_run(&plan, nseg, (uint8_t *)c->dscratch, (uint8_t *)c->hscratch, soff, moff, sval, stream,
+                            c);
         /* statuses land in the pinned mirror's status area (zeroed by the upload) */
         if (!err) err = pncxrt_memcpy_d2h(c->hscratch, c->dscratch, sizeof(int) * (size_t)nseg, stream);
         if (!err) err = spin_wait(c, stream);
+        if (!err && c->timing) batch_time(c);
         if (!err)
             for (i = 0; i < nseg; i++)
                 if (hstat[i] == NC_NOERR) hstat[i] = ((int *)c->hscratch)[i] != 0 ? NC_ERANGE : NC_NOERR;
@@ -1455,6 +1474,39 @@ out:
         }
     free(hstat);
     return err ? (err < 0 ? err : PNCX_EDEVICE) : first;
+}
+
+int pncx_dev_batch_timing(int enable)
+{
+    ctx_t *c;
+    if (!have_device() || (c = get_ctx()) == NULL) return PNCX_EDEVICE;
+    pthread_mutex_lock(&c->lock);
+    if (enable && c->tev0 == NULL &&
+        (pncxrt_event_create(&c->tev0) != 0 || pncxrt_event_create(&c->tev1) != 0)) {
+        pncxrt_event_destroy(c->tev0);
+        c->tev0 = c->tev1 = NULL;
+        pthread_mutex_unlock(&c->lock);
+        return PNCX_EDEVICE;
+    }
+    c->timing = enable != 0;
+    c->tms = 0.0;
+    c->tcalls = 0;
+    pthread_mutex_unlock(&c->lock);
+    return NC_NOERR;
+}
+
+int pncx_dev_batch_kernel_ms(double *total_ms, long long *calls)
+{
+    ctx_t *c;
+    if (total_ms == NULL || calls == NULL) return NC_EINVAL;
+    *total_ms = 0.0;
+    *calls = 0;
+    if (!have_device() || (c = get_ctx()) == NULL) return PNCX_EDEVICE;
+    pthread_mutex_lock(&c->lock);
+    *total_ms = c->tms;
+    *calls = c->tcalls;
+    pthread_mutex_unlock(&c->lock);
+    return NC_NOERR;
 }
 
 int pncx_batch(const pncx_seg *segs, int nseg, int *status_out)

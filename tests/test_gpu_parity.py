@@ -349,6 +349,33 @@ def test_dev_batch_plan_cache_statuses(torch_cuda):
                 assert outs[k].cpu().numpy()[:n * 2].tobytes() == exp, (sizes, rnd, k)
 
 
+def test_dev_batch_kernel_timing(torch_cuda):
+    """pncx_dev_batch_timing: events around the batch kernels of each call
+    (first call plans and uploads, the next ones hit the plan cache); the
+    summed time and call count reset on enable and stop when disabled."""
+    import ctypes
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    L = pncx.lib()
+    sizes = [1 << 16, 1 << 15, 1 << 16]
+    ins = [torch.arange(n, dtype=torch.float32, device="cuda") for n in sizes]
+    outs = [torch.zeros(n * 4, dtype=torch.uint8, device="cuda") for n in sizes]
+    arr = (pncx.Seg * 3)(*[pncx.Seg(T.PNCX_PUT, 5, T.NC_FLOAT, T.ITYPE_FLOAT, n, outs[k].data_ptr(),
+                                    ins[k].data_ptr(), None) for k, n in enumerate(sizes)])
+    st = (ctypes.c_int * 3)()
+    tot, calls = ctypes.c_double(), ctypes.c_longlong()
+    assert L.pncx_dev_batch_timing(1) == 0
+    for _ in range(3):
+        assert L.pncx_dev_batch(arr, 3, st, None) == 0
+    assert L.pncx_dev_batch_kernel_ms(ctypes.byref(tot), ctypes.byref(calls)) == 0
+    assert calls.value == 3 and 0 < tot.value < 1000
+    assert L.pncx_dev_batch_timing(0) == 0
+    assert L.pncx_dev_batch(arr, 3, st, None) == 0
+    assert L.pncx_dev_batch_kernel_ms(ctypes.byref(tot), ctypes.byref(calls)) == 0 and calls.value == 0
+    exp = np.arange(sizes[1], dtype=">f4").tobytes()
+    assert outs[1].cpu().numpy().tobytes() == exp
+
+
 # ------------------------------------------- full-size (BASELINE) properties
 def _splitmix64_torch(torch, n, seed, chunk=1 << 27):
     """splitmix64 stream on the GPU (element i = mix(seed + (i+1)*golden)),

@@ -20,10 +20,13 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-# product kernels -> (bench metric key, algorithmic bytes per element, elements per launch)
+# product kernel name pattern -> (bench metric key, algorithmic bytes per element,
+# elements per launch at bench.py's default sizes: C2 32 GiB of NC_DOUBLE,
+# C3 2^31 NC_INT, C4 256 x 2^20)
 KERNELS = {
-    r"k_stream<pncx::SwapOp<8>": ("swap8", 16),
-    r"k_stream<pncx::GetOp<4, 9>": ("get_int_double", 12),
+    r"k_tile<pncx::SwapOp<8>": ("swap8", 16, 1 << 32),
+    r"k_tile<pncx::GetOp<4, 9>": ("get_int_double", 12, 1 << 31),
+    r"k_batch_swapmix": ("batch_c4", 6, 1 << 28),
 }
 
 
@@ -44,10 +47,9 @@ def main():
             for r in rows(p):
                 if r["Counter_Name"] != ctr:
                     continue
-                for pat, (key, bpe) in KERNELS.items():
+                for pat, (key, bpe, elems) in KERNELS.items():
                     if re.search(re.escape(pat), r["Kernel_Name"]):
-                        grid = int(r["Grid_Size"])
-                        per.setdefault(key, {}).setdefault(ctr, []).append((float(r["Counter_Value"]), grid))
+                        per.setdefault(key, {}).setdefault(ctr, []).append(float(r["Counter_Value"]))
     pmc_rows = []
     traffic = {"_comment": "HBM bytes per element from rocprofv3 PMC passes (FETCH_SIZE doubled for "
                            "gfx950, WRITE_SIZE as is; both KiB); written by tools/pmc_summary.py",
@@ -55,14 +57,10 @@ def main():
     for key, d in per.items():
         if "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
             continue
-        f = sum(v for v, _ in d["FETCH_SIZE"]) / len(d["FETCH_SIZE"])
-        w = sum(v for v, _ in d["WRITE_SIZE"]) / len(d["WRITE_SIZE"])
-        grid = d["FETCH_SIZE"][0][1]
-        bpe = dict(KERNELS.values())[key] if False else [b for k, b in KERNELS.values() if k == key][0]
+        f = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"])
+        w = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"])
+        bpe, elems = [(b, e) for k, b, e in KERNELS.values() if k == key][0]
         hbm = (2 * f + w) * 1024.0
-        # elements per launch: threads * VEC (VEC = 2 for swap8, 4 for int->double)
-        vec = {"swap8": 2, "get_int_double": 4}[key]
-        elems = grid * vec
         traffic["kernels"][key] = {"fetch_kib": f, "write_kib": w, "hbm_bytes_per_launch": hbm,
                                    "elements_per_launch": elems, "bytes_per_elem": hbm / elems,
                                    "algorithmic_bytes_per_elem": bpe,
