@@ -541,7 +541,17 @@ struct TransposeGeom {
     int64_t ocount[PNCX_MAX_DIMS], ostride_p[PNCX_MAX_DIMS], ostride_u[PNCX_MAX_DIMS];
 };
 
-template <class Op, bool GATHER>
+template <typename T>
+__device__ __forceinline__ T ld_nt(const uint8_t *p) { return __builtin_nontemporal_load(reinterpret_cast<const T *>(p)); }
+template <typename T>
+__device__ __forceinline__ void st_nt(uint8_t *p, T v) { __builtin_nontemporal_store(v, reinterpret_cast<T *>(p)); }
+
+// ALIGNED: both buffers element-aligned (checked at launch).  Tiles then
+// take an unrolled path whose 16 loads per lane are all issued before the
+// LDS writes, with nontemporal global accesses (tools/transpose_sweep.hip:
+// 3.9 -> 5.7 TB/s for the 64 x 64 tile on the 512x512x128 Fortran-order
+// double case).  Unaligned buffers keep the loops.
+template <class Op, bool GATHER, bool ALIGNED>
 __global__ __launch_bounds__(256) void k_imap_tile(const uint8_t *src, uint8_t *dst, TransposeGeom g,
                                                    typename Op::fill_t fill, int *status) {
     using SU = typename Op::SU;
@@ -567,7 +577,47 @@ __global__ __launch_bounds__(256) void k_imap_tile(const uint8_t *src, uint8_t *
         }
         const int64_t p0 = tp * 64, u0 = tu * 64;
         const int np = (int)(g.cp - p0 < 64 ? g.cp - p0 : 64), nu = (int)(g.cu - u0 < 64 ? g.cu - u0 : 64);
-        if (GATHER) {
+        if (ALIGNED) {
+            // loads unpredicated: indices clamped into the tile, so a partial
+            // tile re-reads valid elements (a predicated load costs a wait per
+            // load: 5.0 -> 4.0 TB/s measured); only the stores are predicated
+            const int cl = lo6 < (GATHER ? nu : np) ? lo6 : (GATHER ? nu : np) - 1;
+            if (GATHER) {
+                TU v[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const int r = hi2 + 4 * i < np ? hi2 + 4 * i : np - 1;
+                    v[i] = ld_nt<TU>(src + (ubase + (p0 + r) * g.ip + (u0 + cl) * g.iu) * UES);
+                }
+#pragma unroll
+                for (int i = 0; i < 16; i++) tile[hi2 + 4 * i][lo6] = v[i];
+                __syncthreads();
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    if (hi2 + 4 * i < nu && lo6 < np) {
+                        uint8_t *pd = dst + (pbase + (u0 + hi2 + 4 * i) * g.su + p0 + lo6) * PES;
+                        DU old = 0;
+                        if constexpr (Op::PRESERVE) old = ld_unaligned<DU>(pd);
+                        st_nt<DU>(pd, Op::one(tile[lo6][hi2 + 4 * i], old, fill, bad));
+                    }
+            } else {
+                SU v[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const int c = hi2 + 4 * i < nu ? hi2 + 4 * i : nu - 1;
+                    v[i] = ld_nt<SU>(src + (pbase + (u0 + c) * g.su + p0 + cl) * PES);
+                }
+                // clamped duplicates convert like the element they copy: no false NC_ERANGE
+#pragma unroll
+                for (int i = 0; i < 16; i++) tile[lo6][hi2 + 4 * i] = Op::one(v[i], DU(0), fill, bad);
+                __syncthreads();
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    if (hi2 + 4 * i < np && lo6 < nu)
+                        st_nt<TU>(dst + (ubase + (p0 + hi2 + 4 * i) * g.ip + (u0 + lo6) * g.iu) * UES,
+                                  tile[hi2 + 4 * i][lo6]);
+            }
+        } else if (GATHER) {
             // user -> LDS, lanes along U
             for (int r = hi2; r < np; r += 4)
                 if (lo6 < nu)
@@ -649,8 +699,16 @@ int launch_imap(const pncxk_args *a, const pncxk_imap *m, int gather) {
     }
     if (transpose_geom(m, &g)) {
         const unsigned grid = (unsigned)(g.ntiles < MAX_BLOCKS ? g.ntiles : MAX_BLOCKS);
-        if (gather) hipLaunchKernelGGL((k_imap_tile<Op, true>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, a->status);
-        else hipLaunchKernelGGL((k_imap_tile<Op, false>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, a->status);
+        const int ues = gather ? Op::SS : Op::DS, pes = gather ? Op::DS : Op::SS;
+        const bool al = (uintptr_t)src % (uintptr_t)(gather ? ues : pes) == 0 &&
+                        (uintptr_t)dst % (uintptr_t)(gather ? pes : ues) == 0;
+        if (gather) {
+            if (al) hipLaunchKernelGGL((k_imap_tile<Op, true, true>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, a->status);
+            else hipLaunchKernelGGL((k_imap_tile<Op, true, false>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, a->status);
+        } else {
+            if (al) hipLaunchKernelGGL((k_imap_tile<Op, false, true>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, a->status);
+            else hipLaunchKernelGGL((k_imap_tile<Op, false, false>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, a->status);
+        }
         return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
     }
     const int grid = launch_grid(a->n, 4);

@@ -103,3 +103,44 @@ def test_imap_rejects_bad_args(torch_cuda):
     imp = (ctypes.c_longlong * 2)(1, 1)
     assert lib.pncx_putn_imap(5, T.NC_INT, xb.ctypes.data, ib.ctypes.data, 2, cnt, imp, T.ITYPE_INT, None) == T.NC_EINVAL
     assert lib.pncx_putn_imap(5, T.NC_INT, xb.ctypes.data, ib.ctypes.data, 17, cnt, imp, T.ITYPE_INT, None) == T.NC_EINVAL
+
+
+@pytest.mark.parametrize("xt,it", [(T.NC_INT, T.ITYPE_DOUBLE), (T.NC_DOUBLE, T.ITYPE_DOUBLE),
+                                   (T.NC_SHORT, T.ITYPE_FLOAT), (T.NC_UINT64, T.ITYPE_SCHAR)])
+@pytest.mark.parametrize("ushift,xshift", [(0, 0), (1, 3), (0, 1), (2, 0)])
+def test_imap_tile_alignment(torch_cuda, xt, it, ushift, xshift):
+    """k_imap_tile takes its nontemporal full-tile path only when both device
+    buffers are element-aligned; byte-shifted buffers take the checked loops.
+    Full 64x64 tiles plus partial edges (130 x 3 x 70, Fortran order)."""
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    ora = OracleConv()
+    count, imap = [130, 3, 70], [1, 130, 390]
+    rng = np.random.default_rng(ushift * 7 + xshift + xt * 3 + it)
+    off = offsets(count, imap)
+    n, span = off.size, int(off.max()) + 1
+    isz, xsz = T.ilen(it), T.xlen(xt)
+    user = np.frombuffer(rng.integers(0, 256, span * isz, dtype=np.uint8).tobytes(), T.ITYPE_NP[it]).copy()
+    if np.issubdtype(user.dtype, np.floating):
+        user = rng.standard_normal(span).astype(user.dtype) * 1e4
+    fill = T.fill_bytes(xt, 42)
+    exp_x, exp_st = ora.putn(5, xt, user[off], it, fill)
+    ubuf = torch.zeros(span * isz + 16, dtype=torch.uint8, device="cuda")
+    ubuf[ushift:ushift + span * isz] = torch.from_numpy(user.view(np.uint8).copy()).cuda()
+    xbuf = torch.zeros(n * xsz + 16, dtype=torch.uint8, device="cuda")
+    du, dx = ubuf[ushift:], xbuf[xshift:]
+    ds = torch.zeros(1, dtype=torch.int32, device="cuda")
+    pncx.dev_putn_imap(5, xt, dx, du, count, imap, it, fill, ds)
+    torch.cuda.synchronize()
+    assert int(ds.item()) == exp_st
+    assert xbuf.cpu().numpy()[xshift:xshift + n * xsz].tobytes() == exp_x
+    # get: convert + scatter back into a shifted copy; gaps keep their bytes
+    vals, gst = ora.getn(5, xt, exp_x, it)
+    exp_user = user.copy()
+    exp_user[off] = vals
+    ubuf[ushift:ushift + span * isz] = torch.from_numpy(user.view(np.uint8).copy()).cuda()
+    ds.zero_()
+    pncx.dev_getn_imap(5, xt, dx, du, count, imap, it, ds)
+    torch.cuda.synchronize()
+    assert int(ds.item()) == gst
+    assert ubuf.cpu().numpy()[ushift:ushift + span * isz].tobytes() == exp_user.view(np.uint8).tobytes()

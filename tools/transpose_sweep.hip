@@ -1,0 +1,169 @@
+// transpose_sweep.hip -- standalone tuning sweep for the varm transpose
+// (k_imap_tile): a Fortran-order user buffer of doubles, count {C0, C1, C2}
+// with imap {1, C0, C0*C1}, packed (C order) with an 8-byte swap.
+//   user  element (u, o, p) at u + o*C0 + p*C0*C1      (U = dim 0, outer = dim 1, P = dim 2)
+//   packed element (u, o, p) at u*C1*C2 + o*C2 + p
+// Not part of the product; the winner is folded into pnetcdf_amd/csrc/
+// pncx_kern.hpp.  Interleaved rounds in one process.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <stdint.h>
+#include <vector>
+#include <algorithm>
+#include <string>
+#include <functional>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+typedef uint64_t u64;
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u64 sw8(u64 v) { return __builtin_bswap64(v); }
+
+struct Geo { long long c0, c1, c2; };
+
+// Tile TP (along P) x TU (along U); VU elements per lane on the user side
+// (lanes along U), VP per lane on the packed side (lanes along P).
+// OB outer indices per block (the same u/p tile for OB consecutive o).
+template <int TP, int TU, int VU, int VP, int BS>
+__global__ __launch_bounds__(BS) void k_tr(const u64 *user, u64 *packed, Geo g) {
+    __shared__ u64 tile[TP][TU + 1];
+    const long long ntu = g.c0 / TU, ntp = g.c2 / TP;
+    long long b = blockIdx.x;
+    const long long tu = b % ntu; b /= ntu;
+    const long long tp = b % ntp; b /= ntp;
+    const long long o = b;
+    const long long u0 = tu * TU, p0 = tp * TP;
+    // read: rows p (TP of them), each TU contiguous user elements; a row takes TU/VU lanes
+    constexpr int LPR = TU / VU;                  // lanes per row
+    constexpr int RPP = BS / LPR;                 // rows per pass
+    constexpr int NR = TP / RPP;                  // passes
+    const int t = threadIdx.x;
+    {
+        const int lr = t % LPR, r0 = t / LPR;
+        u64 v[NR][VU];
+#pragma unroll
+        for (int i = 0; i < NR; i++) {
+            const long long p = p0 + r0 + i * RPP;
+            const u64 *src = user + u0 + lr * VU + o * g.c0 + p * g.c0 * g.c1;
+            if constexpr (VU == 2) {
+                const u64x2 w = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(src));
+                v[i][0] = w.x; v[i][1] = w.y;
+            } else {
+                v[i][0] = __builtin_nontemporal_load(src);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NR; i++)
+#pragma unroll
+            for (int k = 0; k < VU; k++) tile[r0 + i * RPP][lr * VU + k] = v[i][k];
+    }
+    __syncthreads();
+    // write: columns u (TU of them), each TP contiguous packed elements; a column takes TP/VP lanes
+    constexpr int LPC = TP / VP;
+    constexpr int CPP = BS / LPC;
+    constexpr int NC = TU / CPP;
+    {
+        const int lc = t % LPC, c0 = t / LPC;
+#pragma unroll
+        for (int i = 0; i < NC; i++) {
+            const int c = c0 + i * CPP;
+            u64 *dst = packed + (u0 + c) * g.c1 * g.c2 + o * g.c2 + p0 + lc * VP;
+            if constexpr (VP == 2) {
+                u64x2 w;
+                w.x = sw8(tile[lc * 2][c]);
+                w.y = sw8(tile[lc * 2 + 1][c]);
+                __builtin_nontemporal_store(w, reinterpret_cast<u64x2 *>(dst));
+            } else {
+                __builtin_nontemporal_store(sw8(tile[lc][c]), dst);
+            }
+        }
+    }
+}
+
+// the product's current shape: 64 x 64, one element per lane, plain accesses, 256 threads
+__global__ __launch_bounds__(256) void k_cur(const u64 *user, u64 *packed, Geo g) {
+    __shared__ u64 tile[64][65];
+    const long long ntu = g.c0 / 64, ntp = g.c2 / 64;
+    long long b = blockIdx.x;
+    const long long tu = b % ntu; b /= ntu;
+    const long long tp = b % ntp; b /= ntp;
+    const long long o = b;
+    const long long u0 = tu * 64, p0 = tp * 64;
+    const int lo6 = threadIdx.x & 63, hi2 = threadIdx.x >> 6;
+    for (int r = hi2; r < 64; r += 4) tile[r][lo6] = user[u0 + lo6 + o * g.c0 + (p0 + r) * g.c0 * g.c1];
+    __syncthreads();
+    for (int c = hi2; c < 64; c += 4) packed[(u0 + c) * g.c1 * g.c2 + o * g.c2 + p0 + lo6] = sw8(tile[lo6][c]);
+}
+
+__global__ void k_copy(const u64x2 *s, u64x2 *d, long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) { u64x2 w = __builtin_nontemporal_load(s + i); w.x = sw8(w.x); w.y = sw8(w.y); __builtin_nontemporal_store(w, d + i); }
+}
+
+struct Var { std::string name; std::function<void()> run; std::vector<float> ms; };
+
+int main(int argc, char **argv) {
+    const int rounds = argc > 1 ? atoi(argv[1]) : 9;
+    Geo g = {512, 512, 128};
+    if (argc > 4) { g.c0 = atoll(argv[2]); g.c1 = atoll(argv[3]); g.c2 = atoll(argv[4]); }
+    const long long n = g.c0 * g.c1 * g.c2;
+    u64 *user, *packed, *ref;
+    CK(hipMalloc(&user, n * 8));
+    CK(hipMalloc(&packed, n * 8));
+    CK(hipMalloc(&ref, n * 8));
+    std::vector<u64> h(n);
+    for (long long i = 0; i < n; i++) h[i] = (u64)i * 0x9E3779B97F4A7C15ULL;
+    CK(hipMemcpy(user, h.data(), n * 8, hipMemcpyHostToDevice));
+    printf("transpose %lld x %lld x %lld doubles (%.0f MiB each side), rounds %d\n", g.c0, g.c1, g.c2,
+           n * 8 / 1048576.0, rounds);
+    std::vector<Var> vars;
+    auto add = [&](std::string nm, std::function<void()> r) { vars.push_back({nm, r, {}}); };
+    add("current 64x64 v1/v1 bs256", [=] { hipLaunchKernelGGL(k_cur, dim3(n / 4096), dim3(256), 0, 0, user, ref, g); });
+#define TR(TP, TU, VU, VP, BS) add(std::string("tile ") + #TP "x" #TU " vu" #VU " vp" #VP " bs" #BS, [=] { \
+        hipLaunchKernelGGL((k_tr<TP, TU, VU, VP, BS>), dim3(n / (TP * TU)), dim3(BS), 0, 0, user, packed, g); });
+    TR(64, 64, 1, 1, 256) TR(64, 64, 2, 2, 256) TR(64, 128, 2, 2, 256) TR(64, 128, 2, 2, 512) TR(32, 128, 2, 2, 256)
+    TR(128, 64, 2, 2, 256) TR(32, 32, 1, 1, 256) TR(32, 64, 2, 2, 256) TR(64, 64, 2, 2, 512) TR(128, 128, 2, 2, 1024)
+    add("flat swap copy (same bytes)", [=] { hipLaunchKernelGGL(k_copy, dim3(n / 2 / 256), dim3(256), 0, 0,
+                                                                  (const u64x2 *)user, (u64x2 *)packed, n / 2); });
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (auto &v : vars) { v.run(); v.run(); }
+    CK(hipDeviceSynchronize());
+    // correctness: every tiled variant against the current kernel's output
+    std::vector<u64> hr(n), hp(n);
+    CK(hipMemcpy(hr.data(), ref, n * 8, hipMemcpyDeviceToHost));
+    bool ok_ref = true;
+    for (long long u = 0; u < g.c0 && ok_ref; u += 37)
+        for (long long o = 0; o < g.c1 && ok_ref; o += 29)
+            for (long long p = 0; p < g.c2; p++)
+                if (hr[u * g.c1 * g.c2 + o * g.c2 + p] != __builtin_bswap64(h[u + o * g.c0 + p * g.c0 * g.c1])) { ok_ref = false; break; }
+    printf("current kernel vs host transpose: %s\n", ok_ref ? "ok" : "MISMATCH");
+    for (size_t k = 1; k + 1 < vars.size(); k++) {
+        CK(hipMemset(packed, 0, n * 8));
+        vars[k].run();
+        CK(hipMemcpy(hp.data(), packed, n * 8, hipMemcpyDeviceToHost));
+        if (hp != hr) printf("MISMATCH: %s\n", vars[k].name.c_str());
+    }
+    for (int r = 0; r < rounds; r++)
+        for (auto &v : vars) {
+            CK(hipEventRecord(a, 0));
+            v.run();
+            CK(hipEventRecord(b, 0));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            v.ms.push_back(ms);
+        }
+    CK(hipGetLastError());
+    const double moved = 16.0 * n;
+    for (auto &v : vars) {
+        std::sort(v.ms.begin(), v.ms.end());
+        const double med = v.ms[v.ms.size() / 2];
+        printf("%-32s median %7.4f ms  %7.1f GB/s  (%.1f%% of 8 TB/s)\n", v.name.c_str(), med, moved / med / 1e6,
+               100.0 * moved / med / 1e6 / 8000.0);
+    }
+    return 0;
+}
