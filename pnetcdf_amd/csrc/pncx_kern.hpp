@@ -454,7 +454,7 @@ __device__ __forceinline__ int64_t tmap_byte(int64_t j, const pncxk_imap &m) {
     return (int64_t)c * m.textent + m.tdisp[b] + ((int64_t)r - m.tpre[b]) * ES;
 }
 
-// elements per lane in flight in the run-major typemap kernel
+// elements per lane in flight in the gather/scatter kernels
 constexpr int IMAP_U = 4;
 
 // GATHER = true: src strided (user, put); false: dst strided (user, get)
@@ -466,21 +466,35 @@ __global__ __launch_bounds__(256) void k_imap(const uint8_t *src, uint8_t *dst, 
     constexpr int UES = GATHER ? Op::SS : Op::DS;      // user element size
     const int64_t stride = (int64_t)gridDim.x * 256;
     bool bad = false;
-    // (unrolling this loop with the loads first measured slower on the
-    // vector64 / short-run cases, unlike k_tmap_runs below)
-    for (int64_t k = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 + threadIdx.x; k < n; k += stride) {
-        const int64_t j = imap_offset<IDX>((IDX)k, m);          // user element index
-        const int64_t u = m.tmode ? tmap_byte<UES, IDX>(j, m) : j * UES;
-        const uint8_t *ps = GATHER ? src + u : src + k * Op::SS;
-        uint8_t *pd = GATHER ? dst + k * Op::DS : dst + u;
-        DU old = 0;
-        if constexpr (Op::PRESERVE) old = ld_unaligned<DU>(pd);
-        st_unaligned<DU>(pd, Op::one(ld_unaligned<SU>(ps), old, fill, bad));
+    // IMAP_U elements per lane per step (a block step covers IMAP_U x 256
+    // consecutive elements), all loads issued before the first store.  The
+    // loads are unpredicated -- past the end a lane re-reads element n-1 --
+    // since a predicated load costs a wait of its own; stores are predicated.
+    for (int64_t k0 = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 * IMAP_U + threadIdx.x; k0 < n;
+         k0 += stride * IMAP_U) {
+        SU sv[IMAP_U];
+        DU old[IMAP_U];
+        int64_t uo[IMAP_U];
+#pragma unroll
+        for (int i = 0; i < IMAP_U; i++) {
+            const int64_t k = k0 + i * 256 < n ? k0 + i * 256 : n - 1;
+            const int64_t j = imap_offset<IDX>((IDX)k, m);          // user element index
+            uo[i] = m.tmode ? tmap_byte<UES, IDX>(j, m) : j * UES;
+            sv[i] = ld_unaligned<SU>(GATHER ? src + uo[i] : src + k * Op::SS);
+            old[i] = 0;
+            if constexpr (Op::PRESERVE) old[i] = ld_unaligned<DU>(GATHER ? dst + k * Op::DS : dst + uo[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < IMAP_U; i++) {
+            const int64_t k = k0 + i * 256;
+            if (k < n) st_unaligned<DU>(GATHER ? dst + k * Op::DS : dst + uo[i], Op::one(sv[i], old[i], fill, bad));
+        }
     }
     publish_status(status, bad);
 }
 
-// Derived buftype in packed order with long runs (tmode 3): one wave per run
+// Derived buftype in packed order with long runs (tmode 3, or uniform runs
+// of 256..4096 elements, tmode 1): one wave per run
 // piece (pieces of at most PNCX_TMAP_PIECE elements, split at commit), lanes
 // along the piece -- both sides contiguous, no search.  c = copy, b = piece.
 template <class Op, bool GATHER>
@@ -495,21 +509,21 @@ __global__ __launch_bounds__(256) void k_tmap_runs(const uint8_t *src, uint8_t *
     bool bad = false;
     for (int64_t g = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6); g < total; g += nw) {
         const int64_t c = g / m.tnblk, b = g - c * m.tnblk;
-        const int64_t p0 = m.tpre[b], len = m.tpre[b + 1] - p0;
-        const int64_t ub = c * m.textent + m.tdisp[b];    // user byte offset of the piece
+        // uniform runs (tmode 1): run b is elements [b*tlen, (b+1)*tlen) at tdisp0 + b*tstride
+        const int64_t p0 = m.tmode == 1 ? b * m.tlen : m.tpre[b];
+        const int64_t len = m.tmode == 1 ? m.tlen : m.tpre[b + 1] - p0;
+        const int64_t ub = c * m.textent + (m.tmode == 1 ? m.tdisp0 + b * m.tstride : m.tdisp[b]);
         const int64_t kb = c * m.tn + p0;                   // packed element of the piece
-        for (int64_t e0 = lane; e0 < len; e0 += 64 * IMAP_U) {     // loads first, then stores
+        for (int64_t e0 = lane; e0 < len; e0 += 64 * IMAP_U) {     // loads first (clamped), then stores
             SU sv[IMAP_U];
             DU old[IMAP_U];
 #pragma unroll
             for (int i = 0; i < IMAP_U; i++) {
-                const int64_t e = e0 + 64 * i;
-                if (e < len) {
-                    sv[i] = ld_unaligned<SU>(GATHER ? src + ub + e * UES : src + (kb + e) * Op::SS);
-                    old[i] = 0;
-                    if constexpr (Op::PRESERVE)
-                        old[i] = ld_unaligned<DU>(GATHER ? dst + (kb + e) * Op::DS : dst + ub + e * UES);
-                }
+                const int64_t e = e0 + 64 * i < len ? e0 + 64 * i : len - 1;
+                sv[i] = ld_unaligned<SU>(GATHER ? src + ub + e * UES : src + (kb + e) * Op::SS);
+                old[i] = 0;
+                if constexpr (Op::PRESERVE)
+                    old[i] = ld_unaligned<DU>(GATHER ? dst + (kb + e) * Op::DS : dst + ub + e * UES);
             }
 #pragma unroll
             for (int i = 0; i < IMAP_U; i++) {
@@ -690,7 +704,11 @@ int launch_imap(const pncxk_args *a, const pncxk_imap *m, int gather) {
     const typename Op::fill_t fill = (typename Op::fill_t)a->fill;
     hipStream_t st = (hipStream_t)a->stream;
     TransposeGeom g;
-    if (m->tmode == 3) {
+    // run-major: long-run tables in packed order, and uniform runs of 256..4096
+    // elements in packed order (one wave per run instead of a division per
+    // element; with 64-element runs the per-wave setup made it slower:
+    // vector64 5016 -> 3467 GB/s)
+    if (m->tmode == 3 || (m->tmode == 1 && m->ndims == 1 && m->imap[0] == 1 && m->tlen >= 256 && m->tlen <= 4096)) {
         const int64_t pieces = a->n / m->tn * m->tnblk;
         const unsigned grid = (unsigned)((pieces + 3) / 4 < MAX_BLOCKS ? (pieces + 3) / 4 : MAX_BLOCKS);
         if (gather) hipLaunchKernelGGL((k_tmap_runs<Op, true>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, a->status);

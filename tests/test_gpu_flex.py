@@ -192,6 +192,21 @@ def test_flex_long_runs(torch_cuda, where, imap):
 
 
 @pytest.mark.parametrize("where", ["host", "dev"])
+@pytest.mark.parametrize("blen,imap", [(64, False), (256, False), (300, False), (4096, False), (5000, False),
+                                       (300, True)])
+def test_flex_uniform_long_runs(torch_cuda, where, blen, imap):
+    """uniform runs of 256..4096 elements in packed order go one wave per run
+    (k_tmap_runs, tmode 1); shorter or longer runs, or an imap, take k_imap"""
+    nb = 3000 if blen <= 64 else 40
+    disp = (np.arange(nb) * (blen + 16) + 3).tolist()
+    n = nb * blen * 2
+    count, im = ([2, n // 2], [1, 2]) if imap else (None, None)
+    dt = run_case(torch_cuda, where, T.NC_FLOAT, T.ITYPE_DOUBLE, disp, [blen] * nb, nb * (blen + 16) + 5, 2,
+                  count, im, 14 + blen)
+    assert dt.inq()["layout"] == 1
+
+
+@pytest.mark.parametrize("where", ["host", "dev"])
 def test_flex_large_uniform(torch_cuda, where):
     # vector(2^18 blocks of 3, stride 5) x 2 copies
     nb = 1 << 18

@@ -8,6 +8,7 @@ Workloads (NC_DOUBLE external <- double user buffer, put direction):
             subarray buftype, 64516 runs of 254 elements -> general table
   vector2   every other element (MPI_Type_vector(n, 1, 2)) -> uniform runs
   vector64  runs of 64 every 80 -> uniform runs
+  vector256 runs of 256 every 272 -> uniform runs, one wave per run
   transpose varm with imap = Fortran order over a 512 x 512 x 128 request
   contig    plain pncx_dev_putn on the same n (the roofline reference)
 
@@ -71,7 +72,7 @@ def main():
         lambda: lib.pncx_dev_putn(5, T.NC_DOUBLE, ctypes.c_void_p(xb.data_ptr()), ctypes.c_void_p(ub.data_ptr()), n,
                                   T.ITYPE_DOUBLE, fp, ctypes.c_void_p(st.data_ptr()), sp), n))
     # vector2 / vector64 over 2^27 elements
-    for name, blen, stride in (("vector2", 1, 2), ("vector64", 64, 80)):
+    for name, blen, stride in (("vector2", 1, 2), ("vector64", 64, 80), ("vector256", 256, 272)):
         nb = (1 << 27) // blen
         span = nb * stride * 8
         u2 = torch.empty(span, dtype=torch.uint8, device="cuda")
