@@ -286,6 +286,7 @@ typedef struct ctx_t {
      * epoch value, so they need no zeroing) */
     int    epoch;
     int    cache_valid, cache_nseg, cache_ncls;
+    int    cache_swaponly;    /* cached plan holds only swaps/copies: no statuses to read */
     struct pncx_seg *cache_segs;
     struct cls_t *cache_cls;
     size_t cache_soff, cache_moff;
@@ -1385,7 +1386,7 @@ int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_
 {
     ctx_t *c;
     plan_t plan;
-    int *hstat, i, err = 0, first = NC_NOERR, sval, nclassified = 0, unbatched = 0;
+    int *hstat, i, err = 0, first = NC_NOERR, sval, nclassified = 0, unbatched = 0, swaponly = 1;
     if (nseg <= 0) return NC_NOERR;
     if (!have_device()) return PNCX_EDEVICE;
     c = get_ctx();
@@ -1402,11 +1403,14 @@ int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_
         memcmp(c->cache_segs, segs, sizeof(pncx_seg) * (size_t)nseg) == 0) {
         err = launch_classes(c->cache_cls, c->cache_ncls, (uint8_t *)c->dscratch, c->cache_soff, c->cache_moff,
                              sval, 0, stream, c);
-        if (!err) err = pncxrt_memcpy_d2h(c->hscratch, c->dscratch, sizeof(int) * (size_t)nseg, stream);
+        /* byte swaps and copies never raise NC_ERANGE: no status read-back */
+        if (!err && !c->cache_swaponly)
+            err = pncxrt_memcpy_d2h(c->hscratch, c->dscratch, sizeof(int) * (size_t)nseg, stream);
         if (!err) err = spin_wait(c, stream);
         if (!err && c->timing) batch_time(c);
         if (!err)
-            for (i = 0; i < nseg; i++) hstat[i] = ((int *)c->hscratch)[i] == sval ? NC_ERANGE : NC_NOERR;
+            for (i = 0; i < nseg; i++)
+                hstat[i] = !c->cache_swaponly && ((int *)c->hscratch)[i] == sval ? NC_ERANGE : NC_NOERR;
         pthread_mutex_unlock(&c->lock);
         goto out;
     }
@@ -1425,6 +1429,8 @@ int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_
         plan.nit++;
         nclassified++;
     }
+    for (i = 0; i < plan.nit; i++)
+        if (plan.it[i].op.kind != PNCXK_SWAP) swaponly = 0;
     err = batch_plan(&plan);
     for (i = 0; i < plan.nit; i++) {       /* items a class kernel does not cover run alone */
         const bitem_t *bi = &plan.it[i];
@@ -1438,11 +1444,12 @@ int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_
         if (!err)
             err = batch_run(&plan, nseg, (uint8_t *)c->dscratch, (uint8_t *)c->hscratch, soff, moff, sval, stream,
                             c);
-        /* statuses land in the pinned mirror's status area (zeroed by the upload) */
-        if (!err) err = pncxrt_memcpy_d2h(c->hscratch, c->dscratch, sizeof(int) * (size_t)nseg, stream);
+        /* statuses land in the pinned mirror's status area (zeroed by the
+         * upload); a batch of swaps and copies only has nothing to read */
+        if (!err && !swaponly) err = pncxrt_memcpy_d2h(c->hscratch, c->dscratch, sizeof(int) * (size_t)nseg, stream);
         if (!err) err = spin_wait(c, stream);
         if (!err && c->timing) batch_time(c);
-        if (!err)
+        if (!err && !swaponly)
             for (i = 0; i < nseg; i++)
                 if (hstat[i] == NC_NOERR) hstat[i] = ((int *)c->hscratch)[i] != 0 ? NC_ERANGE : NC_NOERR;
         /* keep the plan when every segment runs in a class kernel */
@@ -1457,6 +1464,7 @@ int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_
                 memcpy(cc, plan.cls, sizeof(cls_t) * (size_t)plan.ncls);
                 c->cache_nseg = nseg;
                 c->cache_ncls = plan.ncls;
+                c->cache_swaponly = swaponly;
                 c->cache_soff = soff;
                 c->cache_moff = moff;
                 c->cache_valid = 1;
