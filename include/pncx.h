@@ -309,10 +309,22 @@ typedef struct pncx_seg {
 int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out,
                    pncx_stream_t stream);
 
+/* Asynchronous form: queues the same launches on `stream` and returns
+ * without waiting.  dstatus is a device array of nseg ints that the caller
+ * zeroes; segment i's word becomes NC_ERANGE if it had out-of-range values
+ * (read it after the stream completes, e.g. pncx_dev_status_read).  The
+ * return value reports argument errors (first bad segment) only.  A repeated
+ * segment list with the same dstatus reuses the device plan and touches no
+ * host staging memory, so calls can be queued back to back; a new plan first
+ * waits for the previous async call's stream. */
+int pncx_dev_batch_async(const pncx_seg *segs, int nseg, int *dstatus,
+                         pncx_stream_t stream);
+
 /* Measurement aid (no reference counterpart): with timing enabled, every
  * pncx_dev_batch call on the current device records HIP events on its stream
  * around its batch kernels only (not the descriptor upload, the status copy
- * or the wait).  pncx_dev_batch_kernel_ms returns the summed kernel time and
+ * or the wait; pncx_dev_batch_async calls are not timed).
+ * pncx_dev_batch_kernel_ms returns the summed kernel time and
  * the number of calls timed since pncx_dev_batch_timing(1) (which resets
  * both). */
 int pncx_dev_batch_timing(int enable);

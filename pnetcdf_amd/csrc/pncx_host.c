@@ -287,6 +287,10 @@ typedef struct ctx_t {
     int    epoch;
     int    cache_valid, cache_nseg, cache_ncls;
     int    cache_swaponly;    /* cached plan holds only swaps/copies: no statuses to read */
+    int   *cache_dstatus;     /* statuses of the cached plan: NULL = dscratch (synchronous
+                               * pncx_dev_batch), else the caller's (pncx_dev_batch_async) */
+    void  *async_stream;      /* stream of the last async upload not yet known complete */
+    int    async_pending;
     struct pncx_seg *cache_segs;
     struct cls_t *cache_cls;
     size_t cache_soff, cache_moff;
@@ -1336,10 +1340,9 @@ static int launch_classes(const cls_t *cls, int ncls, uint8_t *dbase, size_t sof
 }
 
 static int batch_run(plan_t *p, int nseg, uint8_t *dbase, uint8_t *hbase, size_t soff, size_t moff,
-                     int sval, void *stream, ctx_t *tc)
+                     int sval, void *stream, ctx_t *tc, int *dstat)
 {
     int k, err = 0;
-    int *dstat = (int *)dbase;
     pncxk_seg *hseg = (pncxk_seg *)(hbase + soff);
     memset(hbase, 0, soff);
     for (k = 0; k < p->nsegd; k++) {
@@ -1382,11 +1385,15 @@ static int spin_wait(ctx_t *c, void *stream)
     return pncxrt_event_sync(c->ev);
 }
 
-int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_t stream)
+/* dstatus == NULL: synchronous pncx_dev_batch (statuses come back to the
+ * host, epoch values in the scratch status words); else pncx_dev_batch_async
+ * (the kernels set the caller's device words to NC_ERANGE; nothing waits) */
+static int dev_batch(const pncx_seg *segs, int nseg, int *status_out, int *dstatus, pncx_stream_t stream)
 {
     ctx_t *c;
     plan_t plan;
     int *hstat, i, err = 0, first = NC_NOERR, sval, nclassified = 0, unbatched = 0, swaponly = 1;
+    const int async = dstatus != NULL;
     if (nseg <= 0) return NC_NOERR;
     if (!have_device()) return PNCX_EDEVICE;
     c = get_ctx();
@@ -1398,21 +1405,30 @@ int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_
      * stay in place, so a repeated segment list needs no upload at all */
     c->epoch = (c->epoch + 1) & 0x3fffffff;
     if (c->epoch == 0) { c->epoch = 1; c->cache_valid = 0; }
-    sval = 0x40000000 | c->epoch;
-    if (c->cache_valid && c->cache_nseg == nseg &&
+    sval = async ? NC_ERANGE : 0x40000000 | c->epoch;
+    if (c->cache_valid && c->cache_nseg == nseg && c->cache_dstatus == dstatus &&
         memcmp(c->cache_segs, segs, sizeof(pncx_seg) * (size_t)nseg) == 0) {
         err = launch_classes(c->cache_cls, c->cache_ncls, (uint8_t *)c->dscratch, c->cache_soff, c->cache_moff,
-                             sval, 0, stream, c);
-        /* byte swaps and copies never raise NC_ERANGE: no status read-back */
-        if (!err && !c->cache_swaponly)
-            err = pncxrt_memcpy_d2h(c->hscratch, c->dscratch, sizeof(int) * (size_t)nseg, stream);
-        if (!err) err = spin_wait(c, stream);
-        if (!err && c->timing) batch_time(c);
-        if (!err)
-            for (i = 0; i < nseg; i++)
-                hstat[i] = !c->cache_swaponly && ((int *)c->hscratch)[i] == sval ? NC_ERANGE : NC_NOERR;
+                             sval, 0, stream, async ? NULL : c);
+        if (!async) {
+            /* byte swaps and copies never raise NC_ERANGE: no status read-back */
+            if (!err && !c->cache_swaponly)
+                err = pncxrt_memcpy_d2h(c->hscratch, c->dscratch, sizeof(int) * (size_t)nseg, stream);
+            if (!err) err = spin_wait(c, stream);
+            if (!err && c->timing) batch_time(c);
+            if (!err)
+                for (i = 0; i < nseg; i++)
+                    hstat[i] = !c->cache_swaponly && ((int *)c->hscratch)[i] == sval ? NC_ERANGE : NC_NOERR;
+        }
         pthread_mutex_unlock(&c->lock);
         goto out;
+    }
+    /* a new plan rewrites the pinned mirror and the device descriptors: an
+     * async call's upload (or its kernels) may still be reading them */
+    if (c->async_pending) {
+        err = pncxrt_stream_sync(c->async_stream);
+        c->async_pending = 0;
+        if (err) { pthread_mutex_unlock(&c->lock); free(hstat); return PNCX_EDEVICE; }
     }
     memset(&plan, 0, sizeof plan);
     plan.it = (bitem_t *)calloc((size_t)nseg, sizeof *plan.it);
@@ -1443,15 +1459,20 @@ int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_
         err = ensure_scratch(c, moff + sizeof(int) * (size_t)plan.map_ints + 16);
         if (!err)
             err = batch_run(&plan, nseg, (uint8_t *)c->dscratch, (uint8_t *)c->hscratch, soff, moff, sval, stream,
-                            c);
-        /* statuses land in the pinned mirror's status area (zeroed by the
-         * upload); a batch of swaps and copies only has nothing to read */
-        if (!err && !swaponly) err = pncxrt_memcpy_d2h(c->hscratch, c->dscratch, sizeof(int) * (size_t)nseg, stream);
-        if (!err) err = spin_wait(c, stream);
-        if (!err && c->timing) batch_time(c);
-        if (!err && !swaponly)
-            for (i = 0; i < nseg; i++)
-                if (hstat[i] == NC_NOERR) hstat[i] = ((int *)c->hscratch)[i] != 0 ? NC_ERANGE : NC_NOERR;
+                            async ? NULL : c, async ? dstatus : (int *)c->dscratch);
+        if (async) {
+            if (!err) { c->async_pending = 1; c->async_stream = stream; }
+        } else {
+            /* statuses land in the pinned mirror's status area (zeroed by the
+             * upload); a batch of swaps and copies only has nothing to read */
+            if (!err && !swaponly)
+                err = pncxrt_memcpy_d2h(c->hscratch, c->dscratch, sizeof(int) * (size_t)nseg, stream);
+            if (!err) err = spin_wait(c, stream);
+            if (!err && c->timing) batch_time(c);
+            if (!err && !swaponly)
+                for (i = 0; i < nseg; i++)
+                    if (hstat[i] == NC_NOERR) hstat[i] = ((int *)c->hscratch)[i] != 0 ? NC_ERANGE : NC_NOERR;
+        }
         /* keep the plan when every segment runs in a class kernel */
         c->cache_valid = 0;
         if (!err && unbatched == 0 && nclassified == nseg) {
@@ -1465,6 +1486,7 @@ int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_
                 c->cache_nseg = nseg;
                 c->cache_ncls = plan.ncls;
                 c->cache_swaponly = swaponly;
+                c->cache_dstatus = dstatus;
                 c->cache_soff = soff;
                 c->cache_moff = moff;
                 c->cache_valid = 1;
@@ -1482,6 +1504,17 @@ out:
         }
     free(hstat);
     return err ? (err < 0 ? err : PNCX_EDEVICE) : first;
+}
+
+int pncx_dev_batch(const pncx_seg *segs, int nseg, int *status_out, pncx_stream_t stream)
+{
+    return dev_batch(segs, nseg, status_out, NULL, stream);
+}
+
+int pncx_dev_batch_async(const pncx_seg *segs, int nseg, int *dstatus, pncx_stream_t stream)
+{
+    if (dstatus == NULL && nseg > 0) return NC_EINVAL;
+    return dev_batch(segs, nseg, NULL, dstatus, stream);
 }
 
 int pncx_dev_batch_timing(int enable)

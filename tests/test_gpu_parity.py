@@ -376,6 +376,93 @@ def test_dev_batch_kernel_timing(torch_cuda):
     assert outs[1].cpu().numpy().tobytes() == exp
 
 
+def test_dev_batch_async(torch_cuda):
+    """pncx_dev_batch_async: the same conversions as the synchronous batch,
+    statuses in the caller's device words (NC_ERANGE or untouched), calls
+    queued back to back on a cached plan, and sync / async calls alternating
+    (each switch re-plans after waiting for the async stream).  Classes:
+    double->NC_SHORT puts (ERANGE-capable), same-type swaps, and one
+    NULL-fill NC_BYTE<-int put that runs outside the class kernels."""
+    import ctypes
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    ora = OracleConv()
+    L = pncx.lib()
+    rng = np.random.default_rng(21)
+    sizes = [5000, 70001, 4096, 123457, 999, 65536]
+    kinds = ["short", "short", "swap", "swap", "byte_null", "short"]
+    fill = np.frombuffer(T.fill_bytes(T.NC_SHORT) + b"\0" * 8, np.uint8).copy()
+    ins, outs, segs = [], [], []
+    for k, (n, kind) in enumerate(zip(sizes, kinds)):
+        if kind == "short":
+            ins.append(torch.zeros(n, dtype=torch.float64, device="cuda"))
+            outs.append(torch.zeros(n * 2 + 16, dtype=torch.uint8, device="cuda"))
+            segs.append(pncx.Seg(T.PNCX_PUT, 5, T.NC_SHORT, T.ITYPE_DOUBLE, n, outs[k].data_ptr(), ins[k].data_ptr(),
+                                 fill.ctypes.data))
+        elif kind == "swap":
+            ins.append(torch.zeros(n, dtype=torch.int32, device="cuda"))
+            outs.append(torch.zeros(n * 4 + 16, dtype=torch.uint8, device="cuda"))
+            segs.append(pncx.Seg(T.PNCX_PUT, 5, T.NC_INT, T.ITYPE_INT, n, outs[k].data_ptr(), ins[k].data_ptr(), None))
+        else:
+            ins.append(torch.zeros(n, dtype=torch.int32, device="cuda"))
+            outs.append(torch.zeros(n + 16, dtype=torch.uint8, device="cuda"))
+            segs.append(pncx.Seg(T.PNCX_PUT, 5, T.NC_BYTE, T.ITYPE_INT, n, outs[k].data_ptr(), ins[k].data_ptr(), None))
+    arr = (pncx.Seg * len(sizes))(*segs)
+    dst = torch.zeros(len(sizes), dtype=torch.int32, device="cuda")
+    hst = (ctypes.c_int * len(sizes))()
+
+    def fresh(rnd):
+        host = []
+        for k, (n, kind) in enumerate(zip(sizes, kinds)):
+            if kind == "short":
+                v = rng.uniform(-30000, 30000, n)
+                if (k + rnd) % 2 == 0:
+                    v[int(rng.integers(0, n))] = 1e9
+            elif kind == "swap":
+                v = rng.integers(-2 ** 31, 2 ** 31, n).astype(np.int32)
+            else:
+                v = rng.integers(-300, 300, n).astype(np.int32)
+            ins[k].copy_(torch.from_numpy(v))
+            outs[k].zero_()
+            host.append(v)
+        return host
+
+    def check(host, statuses):
+        for k, (n, kind) in enumerate(zip(sizes, kinds)):
+            if kind == "short":
+                exp, est = ora.putn(5, T.NC_SHORT, host[k], T.ITYPE_DOUBLE, T.fill_bytes(T.NC_SHORT))
+                nb = n * 2
+            elif kind == "swap":
+                exp, est = ora.putn(5, T.NC_INT, host[k], T.ITYPE_INT, None)
+                nb = n * 4
+            else:
+                exp, est = ora.putn(5, T.NC_BYTE, host[k], T.ITYPE_INT, None, xinit=b"\0" * n)
+                nb = n
+            assert outs[k].cpu().numpy()[:nb].tobytes() == exp, (k, kind)
+            assert statuses[k] == est, (k, kind, statuses[k], est)
+
+    for rnd in range(6):
+        host = fresh(rnd)
+        torch.cuda.synchronize()
+        if rnd % 3 == 2:                           # synchronous call in between: its own plan
+            L.pncx_dev_batch(arr, len(sizes), hst, None)
+            check(host, list(hst))
+        else:
+            dst.zero_()
+            assert L.pncx_dev_batch_async(arr, len(sizes), ctypes.c_void_p(dst.data_ptr()), None) == 0
+            torch.cuda.synchronize()
+            check(host, dst.cpu().tolist())
+    # back to back on the cached plan: the last call's outputs and statuses
+    host = fresh(1)
+    torch.cuda.synchronize()
+    dst.zero_()
+    for _ in range(5):
+        assert L.pncx_dev_batch_async(arr, len(sizes), ctypes.c_void_p(dst.data_ptr()), None) == 0
+    torch.cuda.synchronize()
+    check(host, dst.cpu().tolist())
+    assert L.pncx_dev_batch_async(arr, len(sizes), None, None) == T.NC_EINVAL
+
+
 # ------------------------------------------- full-size (BASELINE) properties
 def _splitmix64_torch(torch, n, seed, chunk=1 << 27):
     """splitmix64 stream on the GPU (element i = mix(seed + (i+1)*golden)),
