@@ -189,6 +189,7 @@ def main():
         splitmix64_fill(torch, buf, SEEDS["c5" if world > 1 else "c2"] + first_rec)
         ptr = ctypes.c_void_p(buf.data_ptr())
         bytes_per_elem = 16                                    # 8 R + 8 W
+        slab_per_elem = 8                                      # external (file) bytes per element
 
         def launch():
             rc = lib.pncx_dev_in_swapn(ptr, n, 8, sptr)
@@ -216,6 +217,7 @@ def main():
             assert rc == 0, rc
         elems = n
         bytes_per_elem = 12
+        slab_per_elem = 4
         metric_key = "get_int_double"
         dtype = "int32->f64"
         cfg = {"workload": "C3: NC_INT on disk read via get_vara_double, fused 4-byte swap + int32->double",
@@ -246,6 +248,7 @@ def main():
             assert rc == 0, rc
         elems = nvar * nel
         bytes_per_elem = 6                                     # avg of 2*2 (short) and 2*4 (float)
+        slab_per_elem = 3
         metric_key = "batch_c4"
         dtype = "i16/f32"
         cfg = {"workload": "C4: iput_vara batch, 256 variables x 2^20 elements, NC_SHORT/NC_FLOAT mixed",
@@ -305,6 +308,7 @@ def main():
         line = {
             "metric": "GiB/s device-resident swap+type-convert, 2/4/8-byte NC arrays",
             "value": round(value, 2),
+            "slab_GiBps": round(value * slab_per_elem / bytes_per_elem, 2),   # external bytes / t
             "unit": "GiB/s",
             "n_gpus": world,
             "steps": args.steps,
