@@ -1,0 +1,189 @@
+"""Reference test programs restated at the file level, one rank, for the
+classic formats the reference loops over (CDF-1, CDF-2, CDF-5):
+
+  test/testcases/test_varm.c   transposed varm reads (iget/get, stride NULL
+                               and not) and transposed schar varm writes
+                               (iput/put); the write buffer must not change
+  test/testcases/flexible.c    flexible puts through hindexed buftypes with
+                               a negative displacement (row swap), with and
+                               without conversion (NC_INT, NC_DOUBLE, NC_BYTE),
+                               fill_var_rec, and gets through a subarray
+                               buftype with ghost cells (blocking and iget)
+  test/testcases/vectors.c     vector(4,3,5) resized to 20 ints, 25 copies,
+                               int -> NC_DOUBLE put_vara and back
+
+The MPI datatypes are given as their flattened typemaps (pncx.DType); the
+MPI flattening itself is checked against MPI_Pack in tests/mpi/flex_check.c.
+Expected values are the ones the reference programs assert (and, where they
+only check return codes, the values their comments print).
+"""
+import numpy as np
+import pytest
+
+from pnetcdf_amd import nctypes as T
+from pnetcdf_amd import ncfile as N
+from pnetcdf_amd import pncx
+
+pytestmark = pytest.mark.gpu
+FORMATS = [("cdf1", 0), ("cdf2", N.NC_64BIT_OFFSET), ("cdf5", N.NC_64BIT_DATA)]
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+    assert torch.cuda.is_available(), "GPU test run without a visible GPU"
+    return torch
+
+
+@pytest.mark.parametrize("fmt,cmode", FORMATS)
+def test_varm(gpu, tmp_path, fmt, cmode):
+    p = str(tmp_path / f"varm_{fmt}.nc")
+    err, ncid = N.create(p, N.NC_CLOBBER | cmode)
+    assert err == 0
+    dims = [N.def_dim(ncid, "Y", 6)[1], N.def_dim(ncid, "X", 4)[1]]
+    err, varid = N.def_var(ncid, "var", T.NC_INT, dims)
+    assert err == 0 and N.enddef(ncid) == 0
+    var = np.arange(24, dtype=np.int32)                      # var[j][i] = j*4+i
+    assert N.put_var(ncid, varid, var, start=[0, 0], count=[6, 4]) == 0
+    assert N.sync(ncid) == 0 and N.close(ncid) == 0
+
+    err, ncid = N.open(p, N.NC_NOWRITE)
+    assert err == 0
+    err, varid = N.inq_varid(ncid, "var")
+    # rh is 4 x 6: rh[j][i] = var[i][j]  (check_read_contents)
+    expect = np.arange(24, dtype=np.float32).reshape(6, 4).T.copy()
+    rh = np.full((4, 6), -1.0, np.float32)
+    err, req = N.iget_var(ncid, varid, rh, start=[0, 0], count=[6, 4], imap=[1, 6])
+    assert err == 0
+    err, st = N.wait_all(ncid, [req])
+    assert err == 0 and st == [0] and np.array_equal(rh, expect)
+    for stride in ([1, 1], None):
+        rh[:] = -1.0
+        assert N.get_var(ncid, varid, rh, start=[0, 0], count=[6, 4], stride=stride, imap=[1, 6]) == 0
+        assert np.array_equal(rh, expect)
+    assert N.close(ncid) == 0
+
+    err, ncid = N.open(p, N.NC_WRITE)
+    assert err == 0
+    assert N.put_var(ncid, varid, np.zeros(24, np.int32), start=[0, 0], count=[6, 4]) == 0
+    varT = (np.arange(24).reshape(4, 6) + 50).astype(np.int8)   # varT[j][i] = j*6+i+50
+    keep = varT.copy()
+    for stride in ([1, 1], None):                               # nonblocking
+        err, req = N.iput_var(ncid, varid, varT, start=[0, 0], count=[6, 4], stride=stride, imap=[1, 6])
+        assert err == 0
+        err, st = N.wait_all(ncid, [req])
+        assert err == 0 and st == [0] and np.array_equal(varT, keep)   # check_write_contents
+    for stride in ([1, 1], None):                               # blocking
+        assert N.put_var(ncid, varid, varT, start=[0, 0], count=[6, 4], stride=stride, imap=[1, 6]) == 0
+        assert np.array_equal(varT, keep)
+    # "ncmpidump -v var": 50, 56, 62, 68 / 51, 57, 63, 69 / ...
+    got = np.empty(24, np.int32)
+    assert N.get_var(ncid, varid, got, start=[0, 0], count=[6, 4]) == 0
+    assert np.array_equal(got.reshape(6, 4), keep.T.astype(np.int32))
+    assert N.close(ncid) == 0
+
+
+NY, NX = 2, 70
+
+
+@pytest.mark.parametrize("fmt,cmode", FORMATS)
+def test_flexible(gpu, tmp_path, fmt, cmode):
+    p = str(tmp_path / f"flexible_{fmt}.nc")
+    err, ncid = N.create(p, N.NC_CLOBBER | cmode)
+    assert err == 0
+    dims = [N.def_dim(ncid, "Y", N.NC_UNLIMITED)[1], N.def_dim(ncid, "X", NX)[1]]
+    v1 = N.def_var(ncid, "var_int", T.NC_INT, dims)[1]
+    v2 = N.def_var(ncid, "var_dbl", T.NC_DOUBLE, dims)[1]
+    v3 = N.def_var(ncid, "var_byte", T.NC_BYTE, dims)[1]
+    assert N.set_fill(ncid, N.NC_FILL)[0] == 0
+    assert N.enddef(ncid) == 0
+    for v in (v1, v2, v3):
+        for rec in (0, 1):
+            assert N.fill_var_rec(ncid, v, rec) == 0
+    buf = np.empty((NY, NX), np.int32)
+    for j in range(NY):
+        buf[j, :] = j + 10                                   # j + rank + 10
+    keep = buf.copy()
+    # hindexed(2, {NX, NX}, {0, buf[0]-buf[1]}, MPI_INT) applied at bufptr = buf[1]: row 1 then row 0
+    swap = pncx.DType(T.ITYPE_INT, [0, -NX * 4], [NX, NX], 2 * NX * 4)
+    for v in (v1, v2):                                       # no conversion, then int -> double
+        assert N.put_var_flex(ncid, v, buf, 1, swap, start=[0, 0], count=[2, NX], base=NX * 4) == 0
+        assert np.array_equal(buf, keep)
+    schar = np.empty(NY * NX, np.int8)
+    for j in range(NY):
+        schar[j * NX:(j + 1) * NX] = j + 10
+    keep_c = schar.copy()
+    swap_c = pncx.DType(T.ITYPE_SCHAR, [0, -NX], [NX, NX], 2 * NX)
+    assert N.put_var_flex(ncid, v3, schar, 1, swap_c, start=[0, 0], count=[2, NX], base=NX) == 0
+    assert np.array_equal(schar, keep_c)
+    schar[:] = -1
+    assert N.get_var_flex(ncid, v3, schar, 1, swap_c, start=[0, 0], count=[2, NX], base=NX) == 0
+    assert np.array_equal(schar, keep_c)
+    assert N.sync(ncid) == 0 and N.close(ncid) == 0
+
+    err, ncid = N.open(p, N.NC_NOWRITE)
+    assert err == 0
+    expect = np.empty((NY, NX), np.int32)
+    expect[0, :], expect[1, :] = 11, 10                      # rows swapped by the buftype
+    for v in (v1, v2):
+        buf[:] = -1
+        assert N.get_var(ncid, v, buf, start=[0, 0], count=[2, NX]) == 0
+        assert np.array_equal(buf, expect)
+    # subarray buftype with 2 ghost cells on each side
+    gy, gx = NY + 4, NX + 4
+    ghost = pncx.DType(T.ITYPE_INT, [((r + 2) * gx + 2) * 4 for r in range(NY)], [NX] * NY, gy * gx * 4)
+    nc = np.full(gy * gx, -1, np.int32)
+    for v in (v1, v2):
+        for nonblocking in (False, True):
+            nc[:] = -1
+            if nonblocking:
+                err, req = N.iget_var_flex(ncid, v, nc, 1, ghost, start=[0, 0], count=[2, NX])
+                assert err == 0
+                err, st = N.wait_all(ncid, [req])
+                assert err == 0 and st == [0]
+            else:
+                assert N.get_var_flex(ncid, v, nc, 1, ghost, start=[0, 0], count=[2, NX]) == 0
+            g = nc.reshape(gy, gx)
+            assert np.array_equal(g[2:2 + NY, 2:2 + NX], expect)
+            inner = np.zeros((gy, gx), bool)
+            inner[2:2 + NY, 2:2 + NX] = True
+            assert (g[~inner] == -1).all()
+    assert N.close(ncid) == 0
+    for d in (swap, swap_c, ghost):
+        d.free()
+
+
+@pytest.mark.parametrize("fmt,cmode", FORMATS)
+def test_vectors(gpu, tmp_path, fmt, cmode):
+    VECCOUNT, BLOCKLEN, STRIDE, COUNT = 4, 3, 5, 25
+    p = str(tmp_path / f"vectors_{fmt}.nc")
+    err, ncid = N.create(p, N.NC_CLOBBER | cmode)
+    assert err == 0
+    err, dimid = N.def_dim(ncid, "50k", 1024 * 50)
+    err, varid = N.def_var(ncid, "vector", T.NC_DOUBLE, [dimid])
+    assert N.def_var_fill(ncid, varid, 0, None) == 0
+    assert N.enddef(ncid) == 0
+    # MPI_Type_vector(4, 3, 5, MPI_INT) resized to 20 ints, 25 copies
+    vec = pncx.DType(T.ITYPE_INT, [b * STRIDE * 4 for b in range(VECCOUNT)], [BLOCKLEN] * VECCOUNT,
+                     STRIDE * VECCOUNT * 4)
+    nuser = STRIDE * VECCOUNT * COUNT
+    userbuf = (3.14159 * np.arange(nuser)).astype(np.int32)      # userbuf[i] = pi*i
+    start, acount = 10, COUNT * 12
+    assert N.put_var_flex(ncid, varid, userbuf, COUNT, vec, start=[start], count=[acount]) == 0
+    assert N.sync(ncid) == 0 and N.close(ncid) == 0
+    err, ncid = N.open(p, N.NC_NOWRITE)
+    assert err == 0
+    cmpbuf = np.zeros(nuser, np.int32)
+    assert N.get_var_flex(ncid, varid, cmpbuf, COUNT, vec, start=[start], count=[acount]) == 0
+    # the reference compares i < acount with i % STRIDE < BLOCKLEN; every
+    # typemap element is compared here, and the gaps must stay zero
+    sel = (np.arange(nuser) % STRIDE) < BLOCKLEN
+    assert np.array_equal(cmpbuf[sel], userbuf[sel]) and not cmpbuf[~sel].any()
+    # on disk: the packed elements as doubles, fill value around them
+    got = np.empty(1024 * 50, np.float64)
+    assert N.get_var(ncid, varid, got) == 0
+    assert np.array_equal(got[start:start + acount], userbuf[sel].astype(np.float64))
+    assert (got[:start] == T.XTYPE_FILL[T.NC_DOUBLE]).all()
+    assert (got[start + acount:] == T.XTYPE_FILL[T.NC_DOUBLE]).all()
+    assert N.close(ncid) == 0
+    vec.free()
