@@ -1137,12 +1137,16 @@ static int cmp_item(const void *pa, const void *pb)
     return a->idx - b->idx;
 }
 
+/* elements before both pointers are aligned: to a 128-byte line when one
+ * head reaches it for both, else the widest of 64/32/16 bytes (vec_head) */
 static long long seg_head(const void *src, const void *dst, int ss, int ds, long long n)
 {
     const uintptr_t s = (uintptr_t)src, d = (uintptr_t)dst;
+    uintptr_t al;
     long long h;
-    for (h = 0; h < 16 && h <= n; h++)
-        if (((s + (uintptr_t)h * ss) & 15) == 0 && ((d + (uintptr_t)h * ds) & 15) == 0) return h;
+    for (al = 128; al >= 16; al >>= 1)
+        for (h = 0; h < 128 && h <= n; h++)
+            if (((s + (uintptr_t)h * ss) & (al - 1)) == 0 && ((d + (uintptr_t)h * ds) & (al - 1)) == 0) return h;
     return -1;
 }
 

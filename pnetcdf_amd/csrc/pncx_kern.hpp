@@ -744,12 +744,15 @@ int launch_imap(const pncxk_args *a, const pncxk_imap *m, int gather) {
 // ---------------------------------------------------------------------------
 // host-side helpers
 // ---------------------------------------------------------------------------
-// Elements before both pointers are 16B-aligned; -1 if no such split exists.
+// Elements before both pointers are aligned, to a 128-byte line when one
+// head puts both there (each wave's 1 KiB then covers whole lines), else to
+// the widest of 64/32/16 bytes; -1 if not even 16 bytes is reachable.
 template <class Op>
 inline int64_t vec_head(const void *src, const void *dst, int64_t n) {
     const uintptr_t s = (uintptr_t)src, d = (uintptr_t)dst;
-    for (int64_t h = 0; h < 16 && h <= n; h++)
-        if (((s + h * Op::SS) & 15) == 0 && ((d + h * Op::DS) & 15) == 0) return h;
+    for (uintptr_t al = 128; al >= 16; al >>= 1)
+        for (int64_t h = 0; h < 128 && h <= n; h++)
+            if (((s + h * Op::SS) & (al - 1)) == 0 && ((d + h * Op::DS) & (al - 1)) == 0) return h;
     return -1;
 }
 

@@ -88,7 +88,7 @@ extern "C" int pncxk_swap_generic(int esize, const pncxk_args *a) {
 // fill_var_buf (ncmpio_fill.c:89-140): replicate one xsize-byte external
 // (big-endian) fill value over the buffer.  Pure write: one-shot grid, one
 // nontemporal 16 B store per lane (16 is a multiple of every xsize), scalar
-// bytes before the first 16 B boundary and after the last.
+// bytes before the first 128 B boundary and after the last 16 B vector.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_fill(uint8_t *dst, int64_t nbytes, int64_t head, int64_t nvec,
                                               u32x4 pattern, uint64_t xvalue, int xsize) {
@@ -111,7 +111,10 @@ extern "C" int pncxk_fill(void *dst, long long nelems, int xsize, const void *xv
     memcpy(&xv, xvalue, (size_t)xsize);                  // external bytes, in memory order
     const int64_t nbytes = (int64_t)nelems * xsize;
     const uintptr_t a = (uintptr_t)dst;
-    int64_t head = (int64_t)((16 - (a & 15)) & 15);
+    // the vector body starts on a 128-byte line: with a 16-byte-aligned but
+    // line-misaligned start every wave store splits 9 lines and the rate
+    // drops from 6.96 to 5.49 TB/s (tools/fill_bench.py, 3-byte offset)
+    int64_t head = (int64_t)((128 - (a & 127)) & 127);
     if (head > nbytes) head = nbytes;
     const int64_t nvec = (nbytes - head) / 16;
     uint8_t pb[16];
