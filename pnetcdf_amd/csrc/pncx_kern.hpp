@@ -560,11 +560,72 @@ __device__ __forceinline__ T ld_nt(const uint8_t *p) { return __builtin_nontempo
 template <typename T>
 __device__ __forceinline__ void st_nt(uint8_t *p, T v) { __builtin_nontemporal_store(v, reinterpret_cast<T *>(p)); }
 
-// ALIGNED: both buffers element-aligned (checked at launch).  Tiles then
-// take an unrolled path whose 16 loads per lane are all issued before the
-// LDS writes, with nontemporal global accesses (tools/transpose_sweep.hip:
-// 3.9 -> 5.7 TB/s for the 64 x 64 tile on the 512x512x128 Fortran-order
-// double case).  Unaligned buffers keep the loops.
+// One 64 x 64 tile, both buffers element-aligned: the 16 loads per lane go
+// out before anything is stored, with nontemporal global accesses, and per-
+// lane addresses advance by a fixed row / column stride.  FULL tiles need no
+// bounds; in a partial tile the load indices are clamped into the tile, so
+// the extra lanes re-read (and convert) valid elements and only the stores
+// are predicated -- a predicated load costs a wait of its own (5.0 -> 4.0
+// TB/s measured).
+template <class Op, bool GATHER, bool FULL, typename TU>
+__device__ __forceinline__ void xpose_tile(const uint8_t *src, uint8_t *dst, const TransposeGeom &g, int64_t pbase,
+                                           int64_t ubase, int64_t p0, int64_t u0, int np, int nu,
+                                           TU (*tile)[65], typename Op::fill_t fill, bool &bad) {
+    using SU = typename Op::SU;
+    using DU = typename Op::DU;
+    constexpr int UES = GATHER ? Op::SS : Op::DS;
+    constexpr int PES = GATHER ? Op::DS : Op::SS;
+    const int lo6 = threadIdx.x & 63, hi2 = threadIdx.x >> 6;
+    const int64_t rs = g.ip * UES, cs = g.su * PES;        // bytes between rows p (user), columns u (packed)
+    if constexpr (GATHER) {
+        const int cl = FULL || lo6 < nu ? lo6 : nu - 1;
+        const uint8_t *s0 = src + (ubase + p0 * g.ip + (u0 + cl) * g.iu) * UES;
+        TU v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int r = FULL || hi2 + 4 * i < np ? hi2 + 4 * i : np - 1;
+            v[i] = ld_nt<TU>(s0 + r * rs);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) tile[hi2 + 4 * i][lo6] = v[i];
+        __syncthreads();
+        uint8_t *d0 = dst + (pbase + u0 * g.su + p0 + lo6) * PES;
+        DU o[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            DU old = 0;
+            if constexpr (Op::PRESERVE)
+                if (FULL || (hi2 + 4 * i < nu && lo6 < np)) old = ld_unaligned<DU>(d0 + (hi2 + 4 * i) * cs);
+            o[i] = Op::one(tile[lo6][hi2 + 4 * i], old, fill, bad);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            if (FULL || (hi2 + 4 * i < nu && lo6 < np)) st_nt<DU>(d0 + (hi2 + 4 * i) * cs, o[i]);
+    } else {
+        const int pl = FULL || lo6 < np ? lo6 : np - 1;
+        const uint8_t *s0 = src + (pbase + u0 * g.su + p0 + pl) * PES;
+        SU v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int c = FULL || hi2 + 4 * i < nu ? hi2 + 4 * i : nu - 1;
+            v[i] = ld_nt<SU>(s0 + c * cs);
+        }
+        // clamped duplicates convert like the element they copy: no false NC_ERANGE
+#pragma unroll
+        for (int i = 0; i < 16; i++) tile[lo6][hi2 + 4 * i] = Op::one(v[i], DU(0), fill, bad);
+        __syncthreads();
+        uint8_t *d0 = dst + (ubase + p0 * g.ip + (u0 + lo6) * g.iu) * UES;
+        TU o[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) o[i] = tile[hi2 + 4 * i][lo6];
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            if (FULL || (hi2 + 4 * i < np && lo6 < nu)) st_nt<TU>(d0 + (hi2 + 4 * i) * rs, o[i]);
+    }
+}
+
+// ALIGNED: both buffers element-aligned (checked at launch): xpose_tile.
+// Otherwise the bounds-checked loops below with unaligned accesses.
 template <class Op, bool GATHER, bool ALIGNED>
 __global__ __launch_bounds__(256) void k_imap_tile(const uint8_t *src, uint8_t *dst, TransposeGeom g,
                                                    typename Op::fill_t fill, int *status) {
@@ -576,61 +637,41 @@ __global__ __launch_bounds__(256) void k_imap_tile(const uint8_t *src, uint8_t *
     __shared__ TU tile[64][65];
     const int t = threadIdx.x, lo6 = t & 63, hi2 = t >> 6;
     bool bad = false;
+    const bool small = g.ntiles < (1LL << 32);          // tile decode in 32 bits (scalar divisions)
     for (int64_t b = xcd_remap(blockIdx.x, gridDim.x); b < g.ntiles; b += gridDim.x) {
-        int64_t q = b;
-        const int64_t tu = q % g.tu;
-        q /= g.tu;
-        const int64_t tp = q % g.tp;
-        q /= g.tp;
-        int64_t pbase = 0, ubase = 0;
-        for (int d = g.nod - 1; d >= 0; d--) {          // outer dims, innermost last
-            const int64_t i = q % g.ocount[d];
-            q /= g.ocount[d];
-            pbase += i * g.ostride_p[d];
-            ubase += i * g.ostride_u[d];
+        int64_t tu, tp, pbase = 0, ubase = 0;
+        if (small) {
+            uint32_t q = (uint32_t)b;
+            tu = q % (uint32_t)g.tu;
+            q /= (uint32_t)g.tu;
+            tp = q % (uint32_t)g.tp;
+            q /= (uint32_t)g.tp;
+            for (int d = g.nod - 1; d >= 0; d--) {      // outer dims, innermost last
+                const uint32_t i = q % (uint32_t)g.ocount[d];
+                q /= (uint32_t)g.ocount[d];
+                pbase += (int64_t)i * g.ostride_p[d];
+                ubase += (int64_t)i * g.ostride_u[d];
+            }
+        } else {
+            int64_t q = b;
+            tu = q % g.tu;
+            q /= g.tu;
+            tp = q % g.tp;
+            q /= g.tp;
+            for (int d = g.nod - 1; d >= 0; d--) {
+                const int64_t i = q % g.ocount[d];
+                q /= g.ocount[d];
+                pbase += i * g.ostride_p[d];
+                ubase += i * g.ostride_u[d];
+            }
         }
         const int64_t p0 = tp * 64, u0 = tu * 64;
         const int np = (int)(g.cp - p0 < 64 ? g.cp - p0 : 64), nu = (int)(g.cu - u0 < 64 ? g.cu - u0 : 64);
         if (ALIGNED) {
-            // loads unpredicated: indices clamped into the tile, so a partial
-            // tile re-reads valid elements (a predicated load costs a wait per
-            // load: 5.0 -> 4.0 TB/s measured); only the stores are predicated
-            const int cl = lo6 < (GATHER ? nu : np) ? lo6 : (GATHER ? nu : np) - 1;
-            if (GATHER) {
-                TU v[16];
-#pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    const int r = hi2 + 4 * i < np ? hi2 + 4 * i : np - 1;
-                    v[i] = ld_nt<TU>(src + (ubase + (p0 + r) * g.ip + (u0 + cl) * g.iu) * UES);
-                }
-#pragma unroll
-                for (int i = 0; i < 16; i++) tile[hi2 + 4 * i][lo6] = v[i];
-                __syncthreads();
-#pragma unroll
-                for (int i = 0; i < 16; i++)
-                    if (hi2 + 4 * i < nu && lo6 < np) {
-                        uint8_t *pd = dst + (pbase + (u0 + hi2 + 4 * i) * g.su + p0 + lo6) * PES;
-                        DU old = 0;
-                        if constexpr (Op::PRESERVE) old = ld_unaligned<DU>(pd);
-                        st_nt<DU>(pd, Op::one(tile[lo6][hi2 + 4 * i], old, fill, bad));
-                    }
-            } else {
-                SU v[16];
-#pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    const int c = hi2 + 4 * i < nu ? hi2 + 4 * i : nu - 1;
-                    v[i] = ld_nt<SU>(src + (pbase + (u0 + c) * g.su + p0 + cl) * PES);
-                }
-                // clamped duplicates convert like the element they copy: no false NC_ERANGE
-#pragma unroll
-                for (int i = 0; i < 16; i++) tile[lo6][hi2 + 4 * i] = Op::one(v[i], DU(0), fill, bad);
-                __syncthreads();
-#pragma unroll
-                for (int i = 0; i < 16; i++)
-                    if (hi2 + 4 * i < np && lo6 < nu)
-                        st_nt<TU>(dst + (ubase + (p0 + hi2 + 4 * i) * g.ip + (u0 + lo6) * g.iu) * UES,
-                                  tile[hi2 + 4 * i][lo6]);
-            }
+            if (np == 64 && nu == 64)
+                xpose_tile<Op, GATHER, true>(src, dst, g, pbase, ubase, p0, u0, np, nu, tile, fill, bad);
+            else
+                xpose_tile<Op, GATHER, false>(src, dst, g, pbase, ubase, p0, u0, np, nu, tile, fill, bad);
         } else if (GATHER) {
             // user -> LDS, lanes along U
             for (int r = hi2; r < np; r += 4)

@@ -13,6 +13,9 @@
 #include <algorithm>
 #include <string>
 #include <functional>
+#include <string.h>
+
+#include "../pnetcdf_amd/csrc/pncx_kern.hpp"   // the product's k_imap_tile, same process
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
@@ -108,6 +111,12 @@ int main(int argc, char **argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 9;
     Geo g = {512, 512, 128};
     if (argc > 4) { g.c0 = atoll(argv[2]); g.c1 = atoll(argv[3]); g.c2 = atoll(argv[4]); }
+    // the k_tr / k_cur variants here assume whole tiles: any other shape
+    // would index past the buffers (the product kernel handles edges itself)
+    if (g.c0 % 128 || g.c2 % 128 || g.c0 <= 0 || g.c1 <= 0 || g.c2 <= 0) {
+        printf("C0 and C2 must be positive multiples of 128\n");
+        return 2;
+    }
     const long long n = g.c0 * g.c1 * g.c2;
     u64 *user, *packed, *ref;
     CK(hipMalloc(&user, n * 8));
@@ -125,6 +134,20 @@ int main(int argc, char **argv) {
         hipLaunchKernelGGL((k_tr<TP, TU, VU, VP, BS>), dim3(n / (TP * TU)), dim3(BS), 0, 0, user, packed, g); });
     TR(64, 64, 1, 1, 256) TR(64, 64, 2, 2, 256) TR(64, 128, 2, 2, 256) TR(64, 128, 2, 2, 512) TR(32, 128, 2, 2, 256)
     TR(128, 64, 2, 2, 256) TR(32, 32, 1, 1, 256) TR(32, 64, 2, 2, 256) TR(64, 64, 2, 2, 512) TR(128, 128, 2, 2, 1024)
+    {   // the product kernel (aligned path) through its own geometry
+        pncxk_imap m;
+        memset(&m, 0, sizeof m);
+        m.ndims = 3;
+        m.count[0] = g.c0; m.count[1] = g.c1; m.count[2] = g.c2;
+        m.imap[0] = 1; m.imap[1] = g.c0; m.imap[2] = g.c0 * g.c1;
+        m.max_count = g.c0 > g.c1 ? (g.c0 > g.c2 ? g.c0 : g.c2) : (g.c1 > g.c2 ? g.c1 : g.c2);
+        pncx::TransposeGeom tg;
+        if (!pncx::transpose_geom(&m, &tg)) { printf("no transpose geometry\n"); exit(1); }
+        const unsigned grid = (unsigned)tg.ntiles;
+        add("product k_imap_tile (aligned)", [=] {
+            hipLaunchKernelGGL((pncx::k_imap_tile<pncx::SwapOp<8>, true, true>), dim3(grid), dim3(256), 0, 0,
+                               (const uint8_t *)user, (uint8_t *)packed, tg, 0ULL, (int *)nullptr); });
+    }
     add("flat swap copy (same bytes)", [=] { hipLaunchKernelGGL(k_copy, dim3(n / 2 / 256), dim3(256), 0, 0,
                                                                   (const u64x2 *)user, (u64x2 *)packed, n / 2); });
     hipEvent_t a, b;
