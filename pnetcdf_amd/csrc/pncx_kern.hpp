@@ -27,9 +27,44 @@ __device__ __forceinline__ u32x4 ld16(const uint8_t *p) {
     if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
     else return *reinterpret_cast<const u32x4 *>(p);
 }
+// Streaming store: "nt sc1" -- nontemporal, and written through without
+// keeping the line in the XCD's L2 (MI355X_MICROARCH.md: sc1 stores drop
+// the line).  The 32 GiB in-place swap moved 6.82 TB/s this way against
+// 6.61 TB/s with nt alone (tools/swap_sweep.hip, profiles/
+// r01_swap_sweep_store_policy.txt).  No builtin exposes sc1 on a global
+// store, hence the vector-store inline asm; nothing in these kernels reads
+// what it stores, so the compiler's wait counting needs no view of it.
+template <typename T>
+__device__ __forceinline__ void st_stream(uint8_t *p, T v) {
+    if constexpr (sizeof(T) == 16) {
+        u32x4 w;
+        __builtin_memcpy(&w, &v, 16);
+        asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(p), "v"(w) : "memory");
+    } else if constexpr (sizeof(T) == 8) {
+        uint64_t w;
+        __builtin_memcpy(&w, &v, 8);
+        asm volatile("global_store_dwordx2 %0, %1, off nt sc1" ::"v"(p), "v"(w) : "memory");
+    } else if constexpr (sizeof(T) == 4) {
+        uint32_t w;
+        __builtin_memcpy(&w, &v, 4);
+        asm volatile("global_store_dword %0, %1, off nt sc1" ::"v"(p), "v"(w) : "memory");
+    } else if constexpr (sizeof(T) == 2) {
+        uint16_t h;
+        __builtin_memcpy(&h, &v, 2);
+        const uint32_t w = h;
+        asm volatile("global_store_short %0, %1, off nt sc1" ::"v"(p), "v"(w) : "memory");
+    } else {
+        static_assert(sizeof(T) == 1, "1/2/4/8/16-byte stores");
+        uint8_t b;
+        __builtin_memcpy(&b, &v, 1);
+        const uint32_t w = b;
+        asm volatile("global_store_byte %0, %1, off nt sc1" ::"v"(p), "v"(w) : "memory");
+    }
+}
+
 template <bool NT>
 __device__ __forceinline__ void st16(uint8_t *p, u32x4 v) {
-    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+    if constexpr (NT) st_stream<u32x4>(p, v);
     else *reinterpret_cast<u32x4 *>(p) = v;
 }
 
@@ -254,7 +289,7 @@ __device__ __forceinline__ typename VecT<B>::type ldv(const uint8_t *p) {
 template <int B, bool NT>
 __device__ __forceinline__ void stv(uint8_t *p, typename VecT<B>::type v) {
     using V = typename VecT<B>::type;
-    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<V *>(p));
+    if constexpr (NT) st_stream<V>(p, v);
     else *reinterpret_cast<V *>(p) = v;
 }
 
@@ -487,7 +522,16 @@ __global__ __launch_bounds__(256) void k_imap(const uint8_t *src, uint8_t *dst, 
 #pragma unroll
         for (int i = 0; i < IMAP_U; i++) {
             const int64_t k = k0 + i * 256;
-            if (k < n) st_unaligned<DU>(GATHER ? dst + k * Op::DS : dst + uo[i], Op::one(sv[i], old[i], fill, bad));
+            // packed output (put): streaming stores, vector64 5013 -> 5355 GB/s; the
+            // scattered user-side stores (get) and k_tmap_runs' run pieces keep
+            // plain stores -- write-through of lines split between waves cost
+            // the subarray case 24 % (5852 -> 4465 GB/s)
+            if (k < n) {
+                uint8_t *pd = GATHER ? dst + k * Op::DS : dst + uo[i];
+                const DU o = Op::one(sv[i], old[i], fill, bad);
+                if constexpr (GATHER) st_stream<DU>(pd, o);
+                else st_unaligned<DU>(pd, o);
+            }
         }
     }
     publish_status(status, bad);
@@ -558,7 +602,7 @@ struct TransposeGeom {
 template <typename T>
 __device__ __forceinline__ T ld_nt(const uint8_t *p) { return __builtin_nontemporal_load(reinterpret_cast<const T *>(p)); }
 template <typename T>
-__device__ __forceinline__ void st_nt(uint8_t *p, T v) { __builtin_nontemporal_store(v, reinterpret_cast<T *>(p)); }
+__device__ __forceinline__ void st_nt(uint8_t *p, T v) { st_stream<T>(p, v); }
 
 // One 64 x 64 tile, both buffers element-aligned: the 16 loads per lane go
 // out before anything is stored, with nontemporal global accesses, and per-

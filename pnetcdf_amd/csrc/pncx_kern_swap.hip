@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void k_fill(uint8_t *dst, int64_t nbytes, int6
     }
     u32x4 *v = reinterpret_cast<u32x4 *>(dst + head);
     for (int64_t k = xcd_remap(blockIdx.x, nb) * 256 + threadIdx.x; k < nvec; k += nb * 256)
-        __builtin_nontemporal_store(pattern, v + k);
+        st_stream<u32x4>(reinterpret_cast<uint8_t *>(v + k), pattern);
 }
 
 extern "C" int pncxk_fill(void *dst, long long nelems, int xsize, const void *xvalue, void *stream) {

@@ -115,6 +115,33 @@ __global__ __launch_bounds__(BS) void k_one2(u32x4 *p, int64_t nvec) {
 #pragma unroll
     for (int u = 0; u < U; u++) if (base + u * BS < nvec) st<NT>(p + base + u * BS, sw8(v[u]));
 }
+// F: oneshot, U vectors per lane BS apart, loads UNPREDICATED (index clamped
+// to the last vector; a predicated load waits on its own), stores predicated;
+// XCD-contiguous remap; store cache policy SP: 0 nt builtin, 1 plain,
+// 2 "sc1" (drop from L2), 3 "sc0 sc1", 4 "nt sc1" (inline asm vector stores)
+template <int SP>
+__device__ __forceinline__ void st_pol(u32x4 *p, u32x4 v) {
+    if constexpr (SP == 0) __builtin_nontemporal_store(v, p);
+    else if constexpr (SP == 1) *p = v;
+    else if constexpr (SP == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+    else if constexpr (SP == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dwordx4 %0, %1, off nt sc1" :: "v"(p), "v"(v) : "memory");
+}
+template <int U, int BS, int SP>
+__global__ __launch_bounds__(BS) void k_one3(u32x4 *p, int64_t nvec) {
+    int64_t b = blockIdx.x;
+    const int64_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = b % 8;
+    b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+    const int64_t base = b * BS * U + threadIdx.x;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int64_t i = base + u * BS < nvec ? base + u * BS : nvec - 1;
+        v[u] = __builtin_nontemporal_load(p + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) if (base + u * BS < nvec) st_pol<SP>(p + base + u * BS, sw8(v[u]));
+}
 // E: oneshot where each lane does U consecutive vectors (32/64B per lane)
 template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_one_consec(u32x4 *p, int64_t nvec) {
@@ -153,8 +180,11 @@ int main(int argc, char **argv) {
 
 #define ONE2(U, NT, BS, XM) { const int64_t g = (nvec + (int64_t)BS * U - 1) / ((int64_t)BS * U); \
       add(std::string("one2 U") + #U + " nt" + #NT + " bs" + #BS + " xcd" + #XM, 2, [=] { hipLaunchKernelGGL((k_one2<U, NT, BS, XM>), dim3(g), dim3(BS), 0, 0, p, nvec); }); }
-    ONE2(1, true, 256, true) ONE2(1, true, 256, false) ONE2(1, true, 512, true) ONE2(1, true, 512, false)
-    ONE2(1, true, 1024, true) ONE2(1, true, 1024, false) ONE2(2, true, 1024, false) ONE2(2, true, 512, false)
+    ONE2(1, true, 256, true)
+#define ONE3(U, BS, SP) { const int64_t g = (nvec + (int64_t)BS * U - 1) / ((int64_t)BS * U); \
+      add(std::string("one3 U") + #U + " bs" + #BS + " store" + #SP, 2, [=] { hipLaunchKernelGGL((k_one3<U, BS, SP>), dim3(g), dim3(BS), 0, 0, p, nvec); }); }
+    ONE3(1, 256, 0) ONE3(2, 256, 0) ONE3(4, 256, 0) ONE3(2, 512, 0) ONE3(1, 256, 1) ONE3(1, 256, 2)
+    ONE3(1, 256, 3) ONE3(1, 256, 4) ONE3(2, 256, 2)
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
