@@ -54,11 +54,12 @@ __device__ __forceinline__ void st_stream(uint8_t *p, T v) {
         const uint32_t w = h;
         asm volatile("global_store_short %0, %1, off nt sc1" ::"v"(p), "v"(w) : "memory");
     } else {
+        // one byte per lane is half a line per wave instruction: write-through
+        // of partial lines is what sc1 must not see (interleaved 16-B stores
+        // fell from 55 % to 21 % of peak with sc1, tools/conv_sweep.hip), so
+        // bytes keep a plain store
         static_assert(sizeof(T) == 1, "1/2/4/8/16-byte stores");
-        uint8_t b;
-        __builtin_memcpy(&b, &v, 1);
-        const uint32_t w = b;
-        asm volatile("global_store_byte %0, %1, off nt sc1" ::"v"(p), "v"(w) : "memory");
+        __builtin_memcpy(p, &v, 1);
     }
 }
 

@@ -17,7 +17,17 @@ typedef double f64x2 __attribute__((ext_vector_type(2)));
 template <class T, bool NT> __device__ __forceinline__ T ld(const T *p) {
     if constexpr (NT) return __builtin_nontemporal_load(p); else return *p;
 }
+// built twice: plain nt stores, and with -DSC1 "nt sc1" stores (write-through, line not kept in L2)
 template <class T, bool NT> __device__ __forceinline__ void st(T *p, T v) {
+#ifdef SC1
+    if constexpr (NT && sizeof(T) == 16) {
+        asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(p), "v"(v) : "memory");
+        return;
+    } else if constexpr (NT && sizeof(T) == 8) {
+        asm volatile("global_store_dwordx2 %0, %1, off nt sc1" ::"v"(p), "v"(v) : "memory");
+        return;
+    }
+#endif
     if constexpr (NT) __builtin_nontemporal_store(v, p); else *p = v;
 }
 __device__ __forceinline__ double cv(uint32_t be) { return (double)(int32_t)__builtin_bswap32(be); }
