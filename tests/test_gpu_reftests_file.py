@@ -11,6 +11,8 @@ classic formats the reference loops over (CDF-1, CDF-2, CDF-5):
                                buftype with ghost cells (blocking and iget)
   test/testcases/vectors.c     vector(4,3,5) resized to 20 ints, 25 copies,
                                int -> NC_DOUBLE put_vara and back
+  test/testcases/flexible_varm.c  a transposing imap combined with a
+                               subarray buftype with ghost cells
 
 The MPI datatypes are given as their flattened typemaps (pncx.DType); the
 MPI flattening itself is checked against MPI_Pack in tests/mpi/flex_check.c.
@@ -187,3 +189,49 @@ def test_vectors(gpu, tmp_path, fmt, cmode):
     assert (got[start + acount:] == T.XTYPE_FILL[T.NC_DOUBLE]).all()
     assert N.close(ncid) == 0
     vec.free()
+
+
+@pytest.mark.parametrize("fmt,cmode", FORMATS)
+def test_flexible_varm(gpu, tmp_path, fmt, cmode):
+    """test/testcases/flexible_varm.c: a transposing imap ({1, NY} on count
+    {NY, NX}) combined with a subarray buftype of an (NX+4) x (NY+4) int
+    buffer with 2 ghost cells, NC_DOUBLE variable; put/iput leave the buffer
+    unchanged, get/iget fill the interior and leave the ghosts"""
+    ny, nx, gh = 32, 128, 2
+    gx, gy = nx + 2 * gh, ny + 2 * gh                     # buf[NX+2G][NY+2G]
+    sub = pncx.DType(T.ITYPE_INT, [((r + gh) * gy + gh) * 4 for r in range(nx)], [ny] * nx, gx * gy * 4)
+    inner = np.zeros((gx, gy), bool)
+    inner[gh:gh + nx, gh:gh + ny] = True
+    put = np.full((gx, gy), -1, np.int32)                 # INIT_PUT_BUF
+    put[gh:gh + nx, gh:gh + ny] = np.arange(nx * ny, dtype=np.int32).reshape(nx, ny)
+    keep = put.copy()
+    p = str(tmp_path / f"flexible_varm_{fmt}.nc")
+    err, ncid = N.create(p, N.NC_CLOBBER | cmode)
+    assert err == 0
+    dims = [N.def_dim(ncid, "Y", ny)[1], N.def_dim(ncid, "X", nx)[1]]
+    err, varid = N.def_var(ncid, "var", T.NC_DOUBLE, dims)
+    assert err == 0 and N.enddef(ncid) == 0
+    args = dict(start=[0, 0], count=[ny, nx], stride=[1, 1], imap=[1, ny])
+    assert N.put_var_flex(ncid, varid, put, 1, sub, **args) == 0
+    assert np.array_equal(put, keep)                      # CHECK_PUT_BUF
+    err, req = N.iput_var_flex(ncid, varid, put, 1, sub, **args)
+    assert err == 0
+    err, st = N.wait_all(ncid, [req])
+    assert err == 0 and st == [0] and np.array_equal(put, keep)
+    assert N.sync(ncid) == 0
+    # on disk: var[y][x] = packed element x*NY + y (the transposing imap)
+    disk = np.empty(ny * nx, np.float64)
+    assert N.get_var(ncid, varid, disk) == 0
+    assert np.array_equal(disk.reshape(ny, nx), np.arange(nx * ny, dtype=np.float64).reshape(nx, ny).T)
+    for nonblocking in (False, True):
+        got = np.full((gx, gy), -2, np.int32)             # INIT_GET_BUF
+        if nonblocking:
+            err, req = N.iget_var_flex(ncid, varid, got, 1, sub, **args)
+            assert err == 0
+            err, st = N.wait_all(ncid, [req])
+            assert err == 0 and st == [0]
+        else:
+            assert N.get_var_flex(ncid, varid, got, 1, sub, **args) == 0
+        assert np.array_equal(got[inner], keep[inner]) and (got[~inner] == -2).all()   # CHECK_GET_BUF
+    assert N.close(ncid) == 0
+    sub.free()
