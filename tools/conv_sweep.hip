@@ -95,6 +95,27 @@ __global__ __launch_bounds__(256) void kD(const u32x4 *s, f64x2 *d, int64_t nv) 
         if (op < 2 * nv) { f64x2 o = {cv(li[2 * p]), cv(li[2 * p + 1])}; st<f64x2, NT>(d + op, o); }
     }
 }
+// G: LDS-DMA staged: each wave global_load_lds 16 B/lane (1 KiB of ints) into
+// its own LDS slice, waits for it, then 2 x (8-byte LDS read -> 16-byte store)
+// per lane, each store instruction contiguous
+template <bool NT>
+__global__ __launch_bounds__(256) void kG(const u32x4 *s, f64x2 *d, int64_t nv) {
+    __shared__ u32x4 lds[256];
+    const int64_t b = xcd(blockIdx.x, gridDim.x);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t v0 = b * 256 + w * 64;                   // first vector of this wave
+    if (v0 + 63 < nv) {
+        __builtin_amdgcn_global_load_lds((const void *)(s + v0 + lane), (void __attribute__((address_space(3))) *)(lds + w * 64), 16, 0, NT ? 2 : 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t *li = (const uint32_t *)(lds + w * 64);
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int p = k * 64 + lane;                   // pair within the wave (128 pairs)
+            f64x2 o = {cv(li[2 * p]), cv(li[2 * p + 1])};
+            st<f64x2, NT>(d + 2 * v0 + p, o);
+        }
+    }
+}
 // E: 4B load -> 8B store
 template <bool NT>
 __global__ __launch_bounds__(256) void kE(const uint32_t *s, double *d, int64_t n) {
@@ -126,6 +147,8 @@ int main(int argc, char **argv) {
     add("C shfl contiguous nt", [=] { hipLaunchKernelGGL((kC<true>), dim3(gA), dim3(256), 0, 0, (const u32x4 *)s, (f64x2 *)d, nv); });
     add("D LDS staged nt", [=] { hipLaunchKernelGGL((kD<true>), dim3(gA), dim3(256), 0, 0, (const u32x4 *)s, (f64x2 *)d, nv); });
     add("D LDS staged nt0", [=] { hipLaunchKernelGGL((kD<false>), dim3(gA), dim3(256), 0, 0, (const u32x4 *)s, (f64x2 *)d, nv); });
+    add("G LDS-DMA staged nt", [=] { hipLaunchKernelGGL((kG<true>), dim3(gA), dim3(256), 0, 0, (const u32x4 *)s, (f64x2 *)d, nv); });
+    add("G LDS-DMA staged nt0", [=] { hipLaunchKernelGGL((kG<false>), dim3(gA), dim3(256), 0, 0, (const u32x4 *)s, (f64x2 *)d, nv); });
     add("E 4B->8B nt", [=] { hipLaunchKernelGGL((kE<true>), dim3((n + 255) / 256), dim3(256), 0, 0, (const uint32_t *)s, d, n); });
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
