@@ -85,6 +85,49 @@ __global__ __launch_bounds__(BS) void k_tr(const u64 *user, u64 *packed, Geo g) 
     }
 }
 
+// ablation toward the product kernel: the 64 x 64 vu1 tile with
+// F & 1: XCD remap of the block index; F & 2: grid-stride loop with a
+// trailing barrier; F & 4: tile decode by 64-bit runtime divisions over a
+// geometry struct (as TransposeGeom)
+struct G2 { long long ntu, ntp, ntiles, c1c2, c2, c0, c0c1; };
+template <int F>
+__global__ __launch_bounds__(256) void k_tr2(const u64 *user, u64 *packed, G2 g) {
+    __shared__ u64 tile[64][65];
+    const int t = threadIdx.x, lo6 = t & 63, hi2 = t >> 6;
+    long long b0 = blockIdx.x;
+    if (F & 1) {
+        const long long nb = gridDim.x, q = nb >> 3, r = nb & 7, x = b0 & 7;
+        b0 = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b0 >> 3);
+    }
+    for (long long b = b0; b < g.ntiles; b += gridDim.x) {
+        long long tu, tp, o;
+        if (F & 4) {
+            long long q = b;
+            tu = q % g.ntu; q /= g.ntu;
+            tp = q % g.ntp; q /= g.ntp;
+            o = q;
+        } else {
+            const unsigned q = (unsigned)b;
+            tu = q % (unsigned)g.ntu;
+            tp = (q / (unsigned)g.ntu) % (unsigned)g.ntp;
+            o = q / (unsigned)(g.ntu * g.ntp);
+        }
+        const long long u0 = tu * 64, p0 = tp * 64;
+        const u64 *s0 = user + u0 + lo6 + o * g.c0 + p0 * g.c0c1;
+        u64 v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) v[i] = __builtin_nontemporal_load(s0 + (hi2 + 4 * i) * g.c0c1);
+#pragma unroll
+        for (int i = 0; i < 16; i++) tile[hi2 + 4 * i][lo6] = v[i];
+        __syncthreads();
+        u64 *d0 = packed + u0 * g.c1c2 + o * g.c2 + p0 + lo6;
+#pragma unroll
+        for (int i = 0; i < 16; i++) __builtin_nontemporal_store(sw8(tile[lo6][hi2 + 4 * i]), d0 + (hi2 + 4 * i) * g.c1c2);
+        if (!(F & 2)) break;
+        __syncthreads();
+    }
+}
+
 // the product's current shape: 64 x 64, one element per lane, plain accesses, 256 threads
 __global__ __launch_bounds__(256) void k_cur(const u64 *user, u64 *packed, Geo g) {
     __shared__ u64 tile[64][65];
@@ -132,8 +175,12 @@ int main(int argc, char **argv) {
     add("current 64x64 v1/v1 bs256", [=] { hipLaunchKernelGGL(k_cur, dim3(n / 4096), dim3(256), 0, 0, user, ref, g); });
 #define TR(TP, TU, VU, VP, BS) add(std::string("tile ") + #TP "x" #TU " vu" #VU " vp" #VP " bs" #BS, [=] { \
         hipLaunchKernelGGL((k_tr<TP, TU, VU, VP, BS>), dim3(n / (TP * TU)), dim3(BS), 0, 0, user, packed, g); });
-    TR(64, 64, 1, 1, 256) TR(64, 64, 2, 2, 256) TR(64, 128, 2, 2, 256) TR(64, 128, 2, 2, 512) TR(32, 128, 2, 2, 256)
-    TR(128, 64, 2, 2, 256) TR(32, 32, 1, 1, 256) TR(32, 64, 2, 2, 256) TR(64, 64, 2, 2, 512) TR(128, 128, 2, 2, 1024)
+    TR(64, 64, 1, 1, 256)
+    {
+        G2 g2 = {g.c0 / 64, g.c2 / 64, n / 4096, g.c1 * g.c2, g.c2, g.c0, g.c0 * g.c1};
+#define TR2(F) add(std::string("ablation flags ") + #F, [=] { hipLaunchKernelGGL((k_tr2<F>), dim3(n / 4096), dim3(256), 0, 0, user, packed, g2); });
+        TR2(0) TR2(1) TR2(2) TR2(3) TR2(4) TR2(7)
+    }
     {   // the product kernel (aligned path) through its own geometry
         pncxk_imap m;
         memset(&m, 0, sizeof m);
