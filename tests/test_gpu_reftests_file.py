@@ -13,6 +13,8 @@ classic formats the reference loops over (CDF-1, CDF-2, CDF-5):
                                int -> NC_DOUBLE put_vara and back
   test/testcases/flexible_varm.c  a transposing imap combined with a
                                subarray buftype with ghost cells
+  test/testcases/tst_vars_fill.m4  strided puts of every type with fill
+                               mode on: the gaps read back as the fill value
 
 The MPI datatypes are given as their flattened typemaps (pncx.DType); the
 MPI flattening itself is checked against MPI_Pack in tests/mpi/flex_check.c.
@@ -235,3 +237,43 @@ def test_flexible_varm(gpu, tmp_path, fmt, cmode):
         assert np.array_equal(got[inner], keep[inner]) and (got[~inner] == -2).all()   # CHECK_GET_BUF
     assert N.close(ncid) == 0
     sub.free()
+
+
+# NC_TYPE(itype) of the m4 test: schar->NC_BYTE, uchar->NC_UBYTE, ..., the unsigned and 64-bit ones CDF-5 only
+VARS_FILL_TYPES = [(np.int8, T.NC_BYTE, False), (np.uint8, T.NC_UBYTE, True), (np.int16, T.NC_SHORT, False),
+                   (np.uint16, T.NC_USHORT, True), (np.int32, T.NC_INT, False), (np.uint32, T.NC_UINT, True),
+                   (np.float32, T.NC_FLOAT, False), (np.float64, T.NC_DOUBLE, False),
+                   (np.int64, T.NC_INT64, True), (np.uint64, T.NC_UINT64, True)]
+
+
+@pytest.mark.parametrize("fmt,cmode", FORMATS)
+def test_tst_vars_fill(gpu, tmp_path, fmt, cmode):
+    """test/testcases/tst_vars_fill.m4: fill mode on, put_vars with strides
+    2..5 in both dimensions into 16 x 16 variables of every type, get_vara of
+    the whole variable: written points hold the value, every other point the
+    type's default fill value (NC_FILL_VALUE(itype))"""
+    NYF = NXF = 16
+    for dt, xt, cdf5_only in VARS_FILL_TYPES:
+        if cdf5_only and cmode != N.NC_64BIT_DATA:
+            continue
+        p = str(tmp_path / f"vars_fill_{fmt}_{np.dtype(dt).name}.nc")
+        err, ncid = N.create(p, N.NC_CLOBBER | cmode)
+        assert err == 0
+        dims = [N.def_dim(ncid, "Y", NYF)[1], N.def_dim(ncid, "X", NXF)[1]]
+        assert N.set_fill(ncid, N.NC_FILL)[0] == 0
+        varids = [N.def_var(ncid, f"var_{k}", xt, dims)[1] for k in range(4)]
+        assert N.enddef(ncid) == 0
+        for k, v in enumerate(varids):
+            s = 2 + k
+            cnt = [-(-NYF // s), -(-NXF // s)]                  # count++ when NY % stride
+            buf = np.zeros(NYF * NXF, dt)                        # ($1)rank
+            assert N.put_var(ncid, v, buf[:cnt[0] * cnt[1]], start=[0, 0], count=cnt, stride=[s, s]) == 0
+            assert N.sync(ncid) == 0
+            got = np.ones(NYF * NXF, dt)
+            assert N.get_var(ncid, v, got, start=[0, 0], count=[NYF, NXF]) == 0
+            g = got.reshape(NYF, NXF)
+            written = np.zeros((NYF, NXF), bool)
+            written[::s, ::s] = True
+            assert (g[written] == 0).all(), (np.dtype(dt).name, k)
+            assert (g[~written] == dt(T.XTYPE_FILL[xt])).all(), (np.dtype(dt).name, k)
+        assert N.close(ncid) == 0
