@@ -1412,8 +1412,17 @@ static int dev_batch(const pncx_seg *segs, int nseg, int *status_out, int *dstat
     sval = async ? NC_ERANGE : 0x40000000 | c->epoch;
     if (c->cache_valid && c->cache_nseg == nseg && c->cache_dstatus == dstatus &&
         memcmp(c->cache_segs, segs, sizeof(pncx_seg) * (size_t)nseg) == 0) {
-        err = launch_classes(c->cache_cls, c->cache_ncls, (uint8_t *)c->dscratch, c->cache_soff, c->cache_moff,
-                             sval, 0, stream, async ? NULL : c);
+        /* async calls on a cached plan read the device descriptors until they
+         * finish: the next re-plan waits for their stream, so only one stream
+         * may have such calls outstanding -- switching streams drains the old one */
+        if (async && c->async_pending && c->async_stream != stream) err = pncxrt_stream_sync(c->async_stream);
+        if (!err)
+            err = launch_classes(c->cache_cls, c->cache_ncls, (uint8_t *)c->dscratch, c->cache_soff,
+                                 c->cache_moff, sval, 0, stream, async ? NULL : c);
+        if (async && !err) {
+            c->async_pending = 1;
+            c->async_stream = stream;
+        }
         if (!async) {
             /* byte swaps and copies never raise NC_ERANGE: no status read-back */
             if (!err && !c->cache_swaponly)

@@ -460,7 +460,59 @@ def test_dev_batch_async(torch_cuda):
         assert L.pncx_dev_batch_async(arr, len(sizes), ctypes.c_void_p(dst.data_ptr()), None) == 0
     torch.cuda.synchronize()
     check(host, dst.cpu().tolist())
+    # the same plan queued on two streams in turn (the library drains the
+    # first stream before the plan is used from the second)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    host = fresh(2)
+    torch.cuda.synchronize()
+    dst.zero_()
+    for s in (sa, sb, sa):
+        assert L.pncx_dev_batch_async(arr, len(sizes), ctypes.c_void_p(dst.data_ptr()),
+                                      ctypes.c_void_p(s.cuda_stream)) == 0
+    torch.cuda.synchronize()
+    check(host, dst.cpu().tolist())
     assert L.pncx_dev_batch_async(arr, len(sizes), None, None) == T.NC_EINVAL
+
+
+def test_dev_batch_async_cached_two_streams(torch_cuda):
+    """a plan that runs entirely in class kernels is cached: async calls then
+    touch no host memory; queued from two streams in turn (the library drains
+    the first before the plan is used from the second), then a synchronous
+    call (a different plan) after them"""
+    import ctypes
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    ora = OracleConv()
+    L = pncx.lib()
+    rng = np.random.default_rng(22)
+    sizes = [70001, 4096, 123457]
+    fill = np.frombuffer(T.fill_bytes(T.NC_SHORT) + b"\0" * 8, np.uint8).copy()
+    ins = [torch.zeros(n, dtype=torch.float64, device="cuda") for n in sizes]
+    outs = [torch.zeros(n * 2 + 16, dtype=torch.uint8, device="cuda") for n in sizes]
+    arr = (pncx.Seg * 3)(*[pncx.Seg(T.PNCX_PUT, 5, T.NC_SHORT, T.ITYPE_DOUBLE, n, outs[k].data_ptr(),
+                                    ins[k].data_ptr(), fill.ctypes.data) for k, n in enumerate(sizes)])
+    dst = torch.zeros(3, dtype=torch.int32, device="cuda")
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    for rnd in range(3):
+        host = []
+        for k, n in enumerate(sizes):
+            v = rng.uniform(-30000, 30000, n)
+            if k == rnd:
+                v[n // 2] = -1e12
+            ins[k].copy_(torch.from_numpy(v))
+            host.append(v)
+        torch.cuda.synchronize()
+        dst.zero_()
+        torch.cuda.synchronize()
+        for s in (sa, sb, sa, sb):
+            assert L.pncx_dev_batch_async(arr, 3, ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(s.cuda_stream)) == 0
+        torch.cuda.synchronize()
+        assert dst.cpu().tolist() == [T.NC_ERANGE if k == rnd else 0 for k in range(3)]
+        for k, n in enumerate(sizes):
+            exp, _ = ora.putn(5, T.NC_SHORT, host[k], T.ITYPE_DOUBLE, T.fill_bytes(T.NC_SHORT))
+            assert outs[k].cpu().numpy()[:n * 2].tobytes() == exp
+    st = (ctypes.c_int * 3)()
+    assert L.pncx_dev_batch(arr, 3, st, None) == T.NC_ERANGE and list(st) == [0, 0, T.NC_ERANGE]
 
 
 # ------------------------------------------- full-size (BASELINE) properties
