@@ -127,11 +127,11 @@ __device__ __forceinline__ void st_pol(u32x4 *p, u32x4 v) {
     else if constexpr (SP == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(p), "v"(v) : "memory");
     else asm volatile("global_store_dwordx4 %0, %1, off nt sc1" :: "v"(p), "v"(v) : "memory");
 }
-template <int U, int BS, int SP>
+template <int U, int BS, int SP, bool RM = true>
 __global__ __launch_bounds__(BS) void k_one3(u32x4 *p, int64_t nvec) {
     int64_t b = blockIdx.x;
     const int64_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = b % 8;
-    b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+    if (RM) b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
     const int64_t base = b * BS * U + threadIdx.x;
     u32x4 v[U];
 #pragma unroll
@@ -183,8 +183,10 @@ int main(int argc, char **argv) {
     ONE2(1, true, 256, true)
 #define ONE3(U, BS, SP) { const int64_t g = (nvec + (int64_t)BS * U - 1) / ((int64_t)BS * U); \
       add(std::string("one3 U") + #U + " bs" + #BS + " store" + #SP, 2, [=] { hipLaunchKernelGGL((k_one3<U, BS, SP>), dim3(g), dim3(BS), 0, 0, p, nvec); }); }
-    ONE3(1, 256, 0) ONE3(2, 256, 0) ONE3(4, 256, 0) ONE3(2, 512, 0) ONE3(1, 256, 1) ONE3(1, 256, 2)
-    ONE3(1, 256, 3) ONE3(1, 256, 4) ONE3(2, 256, 2)
+    ONE3(1, 256, 0) ONE3(1, 256, 4) ONE3(1, 512, 4) ONE3(1, 1024, 4) ONE3(1, 128, 4) ONE3(2, 256, 4)
+#define ONE3N(U, BS, SP) { const int64_t g = (nvec + (int64_t)BS * U - 1) / ((int64_t)BS * U); \
+      add(std::string("one3 noremap U") + #U + " bs" + #BS + " store" + #SP, 2, [=] { hipLaunchKernelGGL((k_one3<U, BS, SP, false>), dim3(g), dim3(BS), 0, 0, p, nvec); }); }
+    ONE3N(1, 256, 4) ONE3N(1, 1024, 4)
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
