@@ -15,6 +15,10 @@ classic formats the reference loops over (CDF-1, CDF-2, CDF-5):
                                subarray buftype with ghost cells
   test/testcases/tst_vars_fill.m4  strided puts of every type with fill
                                mode on: the gaps read back as the fill value
+  test/testcases/test_fillvalue.c  _FillValue type rules, a scalar variable
+                               filled with its _FillValue
+  test/testcases/tst_def_var_fill.c  per-variable fill mode, NC_EGLOBAL
+  test/testcases/scalar.c      every put/get form on a scalar variable
 
 The MPI datatypes are given as their flattened typemaps (pncx.DType); the
 MPI flattening itself is checked against MPI_Pack in tests/mpi/flex_check.c.
@@ -277,3 +281,98 @@ def test_tst_vars_fill(gpu, tmp_path, fmt, cmode):
             assert (g[written] == 0).all(), (np.dtype(dt).name, k)
             assert (g[~written] == dt(T.XTYPE_FILL[xt])).all(), (np.dtype(dt).name, k)
         assert N.close(ncid) == 0
+
+
+@pytest.mark.parametrize("fmt,cmode", FORMATS)
+def test_fillvalue(gpu, tmp_path, fmt, cmode):
+    """test/testcases/test_fillvalue.c: a global _FillValue of any type is
+    allowed; a variable's must have the variable's type (NC_EBADTYPE); the
+    scalar NC_INT variable, never written, reads back its _FillValue 5678"""
+    p = str(tmp_path / f"fillvalue_{fmt}.nc")
+    err, ncid = N.create(p, N.NC_CLOBBER | cmode)
+    assert err == 0
+    assert N.put_att(ncid, N.NC_GLOBAL, "_FillValue", T.NC_FLOAT, np.array([1.234], np.float32)) == 0
+    err, varid = N.def_var(ncid, "var", T.NC_INT, [])
+    assert err == 0
+    assert N.put_att(ncid, varid, "_FillValue", T.NC_FLOAT, np.array([1.234], np.float32)) == N.NC_EBADTYPE
+    assert N.put_att(ncid, varid, "_FillValue", T.NC_INT, np.array([5678], np.int32)) == 0
+    assert N.set_fill(ncid, N.NC_FILL)[0] == 0
+    assert N.close(ncid) == 0                               # enddef through close
+    err, ncid = N.open(p, N.NC_NOWRITE)
+    assert err == 0
+    got = np.zeros(1, np.int32)
+    assert N.get_var(ncid, varid, got) == 0 and got[0] == 5678
+    assert N.close(ncid) == 0
+
+
+@pytest.mark.parametrize("fmt,cmode", FORMATS)
+def test_tst_def_var_fill(gpu, tmp_path, fmt, cmode):
+    """test/testcases/tst_def_var_fill.c, one rank: def_var_fill on NC_GLOBAL
+    is NC_EGLOBAL; var_nofill and var_fill get columns 2..3 of an NY x NX
+    NC_INT variable; var_fill reads NC_FILL_INT everywhere else"""
+    ny, nx, rank = 8, 5, 0
+    p = str(tmp_path / f"def_var_fill_{fmt}.nc")
+    err, ncid = N.create(p, N.NC_CLOBBER | cmode)
+    assert err == 0
+    dims = [N.def_dim(ncid, "Y", ny)[1], N.def_dim(ncid, "X", nx)[1]]
+    v0 = N.def_var(ncid, "var_nofill", T.NC_INT, dims)[1]
+    v1 = N.def_var(ncid, "var_fill", T.NC_INT, dims)[1]
+    assert N.def_var_fill(ncid, N.NC_GLOBAL, 1, None) == N.NC_EGLOBAL
+    assert N.def_var_fill(ncid, v0, 1, None) == 0
+    assert N.def_var_fill(ncid, v1, 0, None) == 0
+    assert N.enddef(ncid) == 0
+    assert N.fill_var_rec(ncid, N.NC_GLOBAL, 0) == N.NC_EGLOBAL
+    buf = np.full(ny * nx, rank + 5, np.int32)
+    for v in (v0, v1):
+        assert N.put_var(ncid, v, buf[:ny * 2], start=[0, nx * rank + 2], count=[ny, 2]) == 0
+        assert (buf == rank + 5).all()                      # put buffer not altered
+    assert N.sync(ncid) == 0 and N.close(ncid) == 0
+    err, ncid = N.open(p, N.NC_NOWRITE)
+    assert err == 0
+    assert N.inq_var_fill(ncid, N.NC_GLOBAL, np.int32)[0] == N.NC_EGLOBAL
+    cols = np.zeros((ny, nx), bool)
+    cols[:, 2:4] = True
+    for v, filled in ((v0, False), (v1, True)):
+        got = np.full(ny * nx, -1, np.int32)
+        assert N.get_var(ncid, v, got, start=[0, 0], count=[ny, nx]) == 0
+        g = got.reshape(ny, nx)
+        assert (g[cols] == rank + 5).all()
+        if filled:
+            assert (g[~cols] == T.XTYPE_FILL[T.NC_INT]).all()
+    assert N.close(ncid) == 0
+
+
+SCALAR_ARGS = [dict(start=None), dict(start=[1]), dict(start=[1], count=[2]), dict(count=[2]),
+               dict(start=[1], count=None), dict(), dict(start=[1], count=[2], stride=[2]),
+               dict(count=[2], stride=[2]), dict(start=[1], stride=[2]), dict(start=[1], count=[2]),
+               dict(start=[1], count=[2], stride=[2], imap=[2])]
+
+
+@pytest.mark.parametrize("fmt,cmode", FORMATS)
+def test_scalar(gpu, tmp_path, fmt, cmode):
+    """test/testcases/scalar.c: on a scalar variable every put/get form
+    (var1/vara/vars/varm, blocking and nonblocking) succeeds and ignores
+    start, count, stride and imap, NULL or not"""
+    p = str(tmp_path / f"scalar_{fmt}.nc")
+    err, ncid = N.create(p, N.NC_CLOBBER | cmode)
+    assert err == 0
+    err, varid = N.def_var(ncid, "scalar_var", T.NC_INT, [])
+    assert err == 0 and N.enddef(ncid) == 0
+    for k, a in enumerate(SCALAR_ARGS):
+        buf = np.array([k + 1], np.int32)
+        assert N.put_var(ncid, varid, buf, **a) == 0, a
+        err, req = N.iput_var(ncid, varid, buf, **a)
+        assert err == 0, a
+        assert N.wait_all(ncid)[0] == 0
+    assert N.sync(ncid) == 0 and N.close(ncid) == 0
+    err, ncid = N.open(p, N.NC_NOWRITE)
+    assert err == 0
+    err, varid = N.inq_varid(ncid, "scalar_var")
+    for a in SCALAR_ARGS:
+        got = np.zeros(1, np.int32)
+        assert N.get_var(ncid, varid, got, **a) == 0 and got[0] == len(SCALAR_ARGS), a
+        got[0] = 0
+        err, req = N.iget_var(ncid, varid, got, **a)
+        assert err == 0, a
+        assert N.wait_all(ncid)[0] == 0 and got[0] == len(SCALAR_ARGS), a
+    assert N.close(ncid) == 0
