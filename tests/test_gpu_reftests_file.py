@@ -19,6 +19,9 @@ classic formats the reference loops over (CDF-1, CDF-2, CDF-5):
                                filled with its _FillValue
   test/testcases/tst_def_var_fill.c  per-variable fill mode, NC_EGLOBAL
   test/testcases/scalar.c      every put/get form on a scalar variable
+  test/testcases/flexible2.c   subarray buftypes with ghost cells and type
+                               conversion, blocking and nonblocking
+  test/testcases/flexible_var.c  whole-variable flexible put/get/iput/iget
 
 The MPI datatypes are given as their flattened typemaps (pncx.DType); the
 MPI flattening itself is checked against MPI_Pack in tests/mpi/flex_check.c.
@@ -375,4 +378,125 @@ def test_scalar(gpu, tmp_path, fmt, cmode):
         err, req = N.iget_var(ncid, varid, got, **a)
         assert err == 0, a
         assert N.wait_all(ncid)[0] == 0 and got[0] == len(SCALAR_ARGS), a
+    assert N.close(ncid) == 0
+
+
+def subarray(itype, esize, sizes, subsizes, starts):
+    """MPI_Type_create_subarray(2, ..., MPI_ORDER_C) as its flattened typemap"""
+    disp = [((r + starts[0]) * sizes[1] + starts[1]) * esize for r in range(subsizes[0])]
+    return pncx.DType(itype, disp, [subsizes[1]] * subsizes[0], sizes[0] * sizes[1] * esize)
+
+
+def ghost_mask(sizes, subsizes, g):
+    m = np.zeros(sizes, bool)
+    m[g:g + subsizes[0], g:g + subsizes[1]] = True
+    return m
+
+
+@pytest.mark.parametrize("fmt,cmode", FORMATS)
+def test_flexible2(gpu, tmp_path, fmt, cmode):
+    """test/testcases/flexible2.c, one rank: subarray buftypes with 3 ghost
+    cells and type conversion -- int buffer into NC_INT var_zy (blocking
+    put/get), double buffer into NC_FLOAT var_yx (iput/iget + wait)"""
+    nz, ny, nx, g, rank = 5, 5, 70, 3, 0
+    p = str(tmp_path / f"flexible2_{fmt}.nc")
+    err, ncid = N.create(p, N.NC_CLOBBER | cmode)
+    assert err == 0
+    dz, dy, dx = N.def_dim(ncid, "Z", nz)[1], N.def_dim(ncid, "Y", ny)[1], N.def_dim(ncid, "X", nx)[1]
+    v0 = N.def_var(ncid, "var_zy", T.NC_INT, [dz, dy])[1]
+    v1 = N.def_var(ncid, "var_yx", T.NC_FLOAT, [dy, dx])[1]
+    assert N.enddef(ncid) == 0
+
+    sizes, sub = (nz + 2 * g, ny + 2 * g), (nz, ny)
+    st = subarray(T.ITYPE_INT, 4, sizes, sub, (g, g))
+    buf = np.full(sizes, rank + 10, np.int32)
+    args = dict(start=[nz * rank, 0], count=[nz, ny])
+    assert N.put_var_flex(ncid, v0, buf, 1, st, **args) == 0
+    assert (buf == rank + 10).all()
+    assert N.sync(ncid) == 0
+    buf[:] = -1
+    assert N.get_var_flex(ncid, v0, buf, 1, st, **args) == 0
+    m = ghost_mask(sizes, sub, g)
+    assert (buf[m] == rank + 10).all() and (buf[~m] == -1).all()
+    st.free()
+
+    sizes, sub = (ny + 2 * g, nx + 2 * g), (ny, nx)
+    st = subarray(T.ITYPE_DOUBLE, 8, sizes, sub, (g, g))
+    buf = np.full(sizes, rank + 10, np.float64)
+    args = dict(start=[0, nx * rank], count=[ny, nx])
+    err, req = N.iput_var_flex(ncid, v1, buf, 1, st, **args)
+    assert err == 0
+    err, s = N.wait_all(ncid, [req])
+    assert err == 0 and s == [0] and (buf == rank + 10).all()
+    buf[:] = -1
+    err, req = N.iget_var_flex(ncid, v1, buf, 1, st, **args)
+    assert err == 0
+    err, s = N.wait_all(ncid, [req])
+    m = ghost_mask(sizes, sub, g)
+    assert err == 0 and s == [0] and (buf[m] == rank + 10).all() and (buf[~m] == -1).all()
+    st.free()
+    assert N.close(ncid) == 0
+
+
+@pytest.mark.parametrize("fmt,cmode", FORMATS)
+def test_flexible_var(gpu, tmp_path, fmt, cmode):
+    """test/testcases/flexible_var.c, one rank: put_var/get_var/iput_var/
+    iget_var of a whole NY x NX NC_DOUBLE variable through a subarray int
+    buftype with 2 ghost cells (bufcount 1), then with a plain int buffer
+    (the reference's bufcount = NC_COUNT_IGNORE with MPI_INT)"""
+    ny, nx, g = 32, 128, 2
+    p = str(tmp_path / f"flexible_var_{fmt}.nc")
+    err, ncid = N.create(p, N.NC_CLOBBER | cmode)
+    assert err == 0
+    dims = [N.def_dim(ncid, "Y", ny)[1], N.def_dim(ncid, "X", nx)[1]]
+    varid = N.def_var(ncid, "var", T.NC_DOUBLE, dims)[1]
+    assert N.enddef(ncid) == 0
+    sizes, sub = (ny + 2 * g, nx + 2 * g), (ny, nx)
+    st = subarray(T.ITYPE_INT, 4, sizes, sub, (g, g))
+    m = ghost_mask(sizes, sub, g)
+    inner = np.arange(ny * nx, dtype=np.int32)
+
+    def put_buf():                                          # INIT_PUT_BUF_GHOST
+        b = np.full(sizes, -1, np.int32)
+        b[m] = inner
+        return b
+
+    def check_get(b):                                       # CHECK_GET_BUF_GHOST
+        assert np.array_equal(b[m], inner) and (b[~m] == -2).all()
+
+    def get_both():
+        b = np.full(sizes, -2, np.int32)                    # INIT_GET_BUF
+        assert N.get_var_flex(ncid, varid, b, 1, st) == 0
+        check_get(b)
+        b[:] = -2
+        err, req = N.iget_var_flex(ncid, varid, b, 1, st)
+        assert err == 0 and N.wait_all(ncid, [req]) == (0, [0])
+        check_get(b)
+
+    b = put_buf()
+    assert N.put_var_flex(ncid, varid, b, 1, st) == 0
+    assert np.array_equal(b, put_buf())                     # CHECK_PUT_BUF_GHOST
+    get_both()
+    assert N.put_var(ncid, varid, np.zeros(ny * nx, np.int32)) == 0
+    b = put_buf()
+    err, req = N.iput_var_flex(ncid, varid, b, 1, st)
+    assert err == 0 and np.array_equal(b, put_buf())
+    assert N.wait_all(ncid, [req]) == (0, [0])
+    get_both()
+    st.free()
+
+    plain = inner.copy()                                    # no ghost cells
+    assert N.put_var(ncid, varid, plain) == 0 and np.array_equal(plain, inner)
+    for nonblocking in (False, True):
+        got = np.full(ny * nx, -2, np.int32)
+        if nonblocking:
+            err, req = N.iget_var(ncid, varid, got)
+            assert err == 0 and N.wait_all(ncid, [req]) == (0, [0])
+        else:
+            assert N.get_var(ncid, varid, got) == 0
+        assert np.array_equal(got, inner)
+    err, req = N.iput_var(ncid, varid, plain)
+    assert err == 0 and N.wait_all(ncid, [req]) == (0, [0]) and np.array_equal(plain, inner)
+    disk = np.empty(ny * nx, np.float64)
+    assert N.get_var(ncid, varid, disk) == 0 and np.array_equal(disk, inner.astype(np.float64))
     assert N.close(ncid) == 0
