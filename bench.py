@@ -1,6 +1,6 @@
 """bench.py -- device-resident XDR swap / NC type-convert throughput on MI355X.
 
-Default workload (BASELINE.json configs[1] / configs[4]): each rank owns one
+Headline workload (BASELINE.json configs[1] / configs[4]): each rank owns one
 32 GiB contiguous NC_DOUBLE slab -- at N=1 the config-2 get_vara slab, at N>1
 the rank's 32 records (1 GiB each) of the config-5 record variable
 v(time=UNLIMITED, 8192, 16384), records 32g..32g+31 on GPU g -- and a step is
@@ -9,7 +9,20 @@ convert_swap.m4:160-174), one kernel launch.  Records are independent, so the
 slabs shard with no data-path collective (weak scaling); torch.distributed
 (RCCL) is used only for the barrier and the max-over-ranks timing.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4]
+At N=1 the same run then measures the other single-GPU configs, one after
+another with each workload's buffers freed before the next (`workloads` in
+the JSON line; none of them feeds `value`):
+    c3        2^31 NC_INT read as double (fused 4-byte swap + int32->double)
+    c4        256 x 2^20 iput batch, NC_SHORT/NC_FLOAT same-type (pncx_dev_batch)
+    c4_async  the same through pncx_dev_batch_async (statuses stay in HBM)
+    c4_erange SURVEY §8(d)'s secondary variant: the NC_SHORT variables come
+              from float values uniform in [-40000, 40000] (~18% NC_ERANGE + fill)
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c4_async|c4_erange]
+
+--gpus N without a torch.distributed launcher (no WORLD_SIZE in the
+environment) starts N ranks itself: torch.distributed.run as a child
+process, before this process touches the GPU, and exits with its status.
 
 Prints ONE JSON line on rank 0.  `value` = algorithmic bytes moved (read +
 write, 16 B per element) by all ranks / max-over-ranks time, in GiB/s.
@@ -18,6 +31,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,8 +44,35 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 SEEDS = {"c1": 0x5EED0001, "c2": 0x5EED0002, "c3": 0x5EED0003, "c4": 0x5EED0004, "c5": 0x5EED0005}
+EXTRA = ("c3", "c4", "c4_async", "c4_erange")
 
 
+# --------------------------------------------------------------- launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_cmd(argv, nproc, port):
+    """torch.distributed.run command that starts `nproc` ranks of this script
+    with the same arguments (one process per GPU, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(nproc, argv):
+    """Start the N ranks as a child process group and return its exit code.
+    This process has not initialised the GPU (nothing here imports torch.cuda
+    state), and it waits rather than exec'ing."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(launch_cmd(argv, nproc, _free_port()), env=env)
+
+
+# --------------------------------------------------------------- helpers
 def splitmix64_fill(torch, out, seed, chunk=1 << 27):
     """element i = splitmix64(seed + (i+1)*golden), generated on the GPU."""
     n = out.numel()
@@ -42,6 +84,15 @@ def splitmix64_fill(torch, out, seed, chunk=1 << 27):
         z = (z ^ ((z >> 27) & 0x1FFFFFFFFF)) * -7723592293110705685
         out[s:s + m] = z ^ ((z >> 31) & 0x1FFFFFFFF)
         del z
+
+
+def splitmix_uniform(torch, out, seed, lo, hi):
+    """float32 values uniform in [lo, hi) from splitmix64 bits (the top 24)."""
+    bits = torch.empty(out.numel(), dtype=torch.int64, device=out.device)
+    splitmix64_fill(torch, bits, seed)
+    u = ((bits >> 40) & 0xFFFFFF).to(torch.float64) * (1.0 / (1 << 24))
+    out.copy_((lo + (hi - lo) * u).to(torch.float32))
+    del bits, u
 
 
 def cpu_baseline_swap8(budget_s=12.0, slab_bytes=2 << 30):
@@ -96,30 +147,54 @@ def cpu_baseline_swap8_threads(budget_s=4.0, slab_bytes=2 << 30, threads=None):
                       f"in {el:.1f} s (orc_in_swapn, gcc -O2)"}
 
 
-def gather_leg(torch, group, buf, gib, to_cpu=False):
-    """Config 5's optional exchange, timed apart from the conversion rate
-    (SURVEY §8(e)): every rank's first `gib` GiB of converted records are
-    gathered into rank 0 (RCCL gather over xGMI).  Checksums (int64 wrapping
-    sums) of what each rank sent are compared on rank 0 with what arrived."""
+def cpu_baseline_getn(xtype, itype, xsz, isz, budget_s=3.0, n=1 << 26, seed=0):
+    """1-core oracle getn (ncmpii_getn_NC_<X>) on a bounded host sample."""
+    from oracle import oracle as O
+    lib = O.lib()
+    xb = np.frombuffer(np.random.default_rng(seed).bytes(n * xsz), np.uint8).copy()
+    ib = np.empty(n * isz, np.uint8)
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        lib.orc_getn(5, xtype, xb.ctypes.data, ib.ctypes.data, n, itype)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": round((xsz + isz) * n * passes / el / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{n} elements, {passes} orc_getn passes in {el:.1f} s (gcc -O2, 1 thread)"}
+
+
+def gather_leg(torch, group, buf, gib, chunk_gib, to_cpu=False):
+    """Config 5's exchange, timed apart from the conversion rate (SURVEY
+    §8(e)): every rank's first `gib` GiB of converted records are gathered
+    into rank 0 (RCCL gather over xGMI), streamed in chunks of `chunk_gib`
+    GiB per rank through one reused receive buffer, so the whole slab (the
+    config's 224 GiB into rank 0 at N=8) moves without rank 0 holding it.
+    Checksums (int64 wrapping sums) of every chunk each rank sent are
+    compared on rank 0 with what arrived."""
     n = min(buf.numel(), int(gib * GIB) // 8)
-    sl = buf[:n]
-    sums = group.all_gather_int(int(sl.sum().item()))
-    group.gather_slices(sl, to_cpu)                      # warm the communicator
+    step = max(1, min(n, int(chunk_gib * GIB) // 8))
+    chunks = [(s, min(step, n - s)) for s in range(0, n, step)]
+    sums = [group.all_gather_int(int(buf[s:s + m].sum().item())) for s, m in chunks]
+    group.gather_slices(buf[:min(step, n)], to_cpu)          # warm the communicator
     torch.cuda.synchronize()
     group.barrier()
+    arrived = []
     t0 = time.perf_counter()
-    got = group.gather_slices(sl, to_cpu)
+    for k, (s, m) in enumerate(chunks):
+        got = group.gather_slices(buf[s:s + m], to_cpu)
+        if got is not None:              # rank 0: checksum kernels queue behind the gather (~2% of its time)
+            arrived.append([g.sum() for g in got])
+        del got
     torch.cuda.synchronize()
     group.barrier()
     el = group.max([time.perf_counter() - t0])[0]
-    ok = True
-    if got is not None:
-        ok = all(int(g.sum().item()) == s for g, s in zip(got, sums))
-        del got
-    into = (group.world - 1) * n * 8                      # rank 0's own slice is local
+    ok = all(int(a.item()) == want for got_k, sums_k in zip(arrived, sums) for a, want in zip(got_k, sums_k))
+    into = (group.world - 1) * n * 8                         # rank 0's own slice is local
     return {"collective": "gather into rank 0 (RCCL over xGMI)" if not to_cpu else "gather into rank 0 (gloo rehearsal)",
-            "bytes_per_rank": n * 8, "bytes_into_rank0": into, "ms": round(el * 1e3, 3),
-            "GBps_into_rank0": round(into / el / 1e9, 2), "checksums_ok": ok}
+            "bytes_per_rank": n * 8, "bytes_into_rank0": into, "chunk_bytes_per_rank": step * 8,
+            "chunks": len(chunks), "ms": round(el * 1e3, 3), "GBps_into_rank0": round(into / el / 1e9, 2),
+            "checksums_ok": ok, "note": "timed region includes one int64 sum kernel per arrived chunk on rank 0"}
 
 
 def load_traffic(kernel_key, elems_per_launch):
@@ -138,203 +213,320 @@ def load_traffic(kernel_key, elems_per_launch):
         return None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"])
-    ap.add_argument("--slab-gib", type=float, default=32.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--async-batch", action="store_true",
-                    help="c4: pncx_dev_batch_async (statuses stay in HBM, calls queue back to back) "
-                         "instead of the synchronous pncx_dev_batch")
-    ap.add_argument("--gather-gib", type=float, default=1.0,
-                    help="N>1, c2: GiB per rank gathered into rank 0 after the timed region (0 = off)")
-    args = ap.parse_args()
+# --------------------------------------------------------------- workloads
+class Workload:
+    """One single-GPU configuration: buffers in HBM, a launch() = one step,
+    the algorithmic bytes of a step, and a check() of the last step."""
+    lib_timed = False          # kernel time from the library's own events (pncx_dev_batch)
 
+    def check(self):
+        return True
+
+    def free(self):
+        for k in list(vars(self)):
+            if k.startswith("_t"):
+                setattr(self, k, None)
+
+
+class C2Swap(Workload):
+    def __init__(self, torch, lib, sptr, slab_gib, world, rank):
+        from pnetcdf_amd.shard import record_slab
+        n = int(slab_gib * GIB) // 8                           # NC_DOUBLE elements per rank
+        rec_elems = 8192 * 16384                               # one 1 GiB record of v(time, 8192, 16384)
+        nrec_total = (n // rec_elems) * world
+        first_rec, my_recs = record_slab(nrec_total, world, rank)
+        self._tbuf = torch.empty(n, dtype=torch.int64, device="cuda")
+        splitmix64_fill(torch, self._tbuf, SEEDS["c5" if world > 1 else "c2"] + first_rec)
+        ptr = ctypes.c_void_p(self._tbuf.data_ptr())
+        self.launch = lambda: _ok(lib.pncx_dev_in_swapn(ptr, n, 8, sptr))
+        self.elems, self.bytes_per_elem, self.slab_per_elem = n, 16, 8
+        self.metric_key, self.dtype = "swap8", "u64"
+        self.kernel = "k_tile<SwapOp<8>, true>"
+        self.cfg = {"workload": ("C2: 32 GiB contiguous NC_DOUBLE get_vara, in-place 8-byte swap" if world == 1 else
+                                 f"C5: NC_DOUBLE record variable v(time={nrec_total}, 8192, 16384), "
+                                 f"{my_recs} x 1 GiB records per GPU, in-place 8-byte swap"),
+                    "slab_gib_per_gpu": slab_gib, "elements_per_gpu": n, "xtype": "NC_DOUBLE",
+                    "itype": "double", "records_per_gpu": my_recs,
+                    "parallelism": f"records sharded one slab per GPU x{world}, no data-path collective"}
+
+
+class C3IntDouble(Workload):
+    def __init__(self, torch, lib, sptr, rank=0):
+        from pnetcdf_amd import nctypes as T
+        n = 1 << 31                                            # NC_INT elements
+        self._txb = torch.empty(n // 2, dtype=torch.int64, device="cuda")
+        splitmix64_fill(torch, self._txb, SEEDS["c3"] + rank)
+        self._tib = torch.empty(n, dtype=torch.float64, device="cuda")
+        self._tst = torch.zeros(1, dtype=torch.int32, device="cuda")
+        px, pi, ps = (ctypes.c_void_p(t.data_ptr()) for t in (self._txb, self._tib, self._tst))
+        self.launch = lambda: _ok(lib.pncx_dev_getn(5, T.NC_INT, px, pi, n, T.ITYPE_DOUBLE, ps, sptr))
+        self.elems, self.bytes_per_elem, self.slab_per_elem = n, 12, 4
+        self.metric_key, self.dtype = "get_int_double", "int32->f64"
+        self.kernel = "k_tile<GetOp<NC_INT, double>, true>"
+        self.cfg = {"workload": "C3: NC_INT on disk read via get_vara_double, fused 4-byte swap + int32->double",
+                    "elements_per_gpu": n, "xtype": "NC_INT", "itype": "double"}
+        self._n = n
+        self._torch = torch
+
+    def check(self):
+        """int->double is exact and never ERANGE: sampled elements equal the
+        byte-reversed int32 of the input, the status word stays NC_NOERR"""
+        torch = self._torch
+        idx = torch.randint(0, self._n, (4096,), device="cuda")
+        xi = self._txb.view(torch.int32)[idx]
+        b = xi.view(torch.uint8).view(-1, 4).flip(1).contiguous().view(torch.int32).view(-1)
+        return bool(torch.equal(b.to(torch.float64), self._tib[idx])) and int(self._tst.item()) == 0
+
+
+class C4Batch(Workload):
+    """256 iput_vara requests of 2^20 elements, flushed by one wait_all: one
+    batched conversion (pncx_dev_batch / pncx_dev_batch_async).  erange:
+    the NC_SHORT variables take float input in [-40000, 40000]."""
+
+    def __init__(self, torch, lib, sptr, mode="sync", rank=0):
+        from pnetcdf_amd import nctypes as T
+        from pnetcdf_amd import pncx
+        nvar, nel = 256, 1 << 20
+        segs, self._tkeep, self._fills = [], [], []
+        self._erange = mode == "erange"
+        for v in range(nvar):
+            if v % 2 == 0 and self._erange:
+                xt, it, isz = T.NC_SHORT, T.ITYPE_FLOAT, 4
+                ib = torch.empty(nel, dtype=torch.float32, device="cuda")
+                splitmix_uniform(torch, ib, SEEDS["c4"] + 1000 * rank + v, -40000.0, 40000.0)
+            else:
+                xt, it, isz = (T.NC_SHORT, T.ITYPE_SHORT, 2) if v % 2 == 0 else (T.NC_FLOAT, T.ITYPE_FLOAT, 4)
+                ib = torch.empty(nel * isz // 8, dtype=torch.int64, device="cuda")
+                splitmix64_fill(torch, ib, SEEDS["c4"] + 1000 * rank + v)
+            xb = torch.empty(nel * T.xlen(xt), dtype=torch.uint8, device="cuda")
+            self._tkeep += [ib, xb]
+            fill = np.frombuffer(T.fill_bytes(xt) + b"\0" * 8, np.uint8).copy()   # native order, 8-byte slot
+            self._fills.append(fill)
+            segs.append(pncx.Seg(T.PNCX_PUT, 5, xt, it, nel, xb.data_ptr(), ib.data_ptr(), fill.ctypes.data))
+        self._arr = (pncx.Seg * nvar)(*segs)
+        self._stv = (ctypes.c_int * nvar)()
+        self._tdst = torch.zeros(nvar, dtype=torch.int32, device="cuda")
+        dstp = ctypes.c_void_p(self._tdst.data_ptr())
+        self._async = mode == "async"
+        self._T, self._nvar, self._torch, self._lib = T, nvar, torch, lib
+        arr, stv = self._arr, self._stv
+        if self._async:
+            self.launch = lambda: _ok(lib.pncx_dev_batch_async(arr, nvar, dstp, sptr))
+        else:
+            self.launch = lambda: _ok(lib.pncx_dev_batch(arr, nvar, stv, sptr), T.NC_ERANGE if self._erange else 0)
+            self.lib_timed = True
+        # algorithmic bytes: isz + xsz per element, summed over the variables
+        per_pair = (4 + 2) + (4 + 4) if self._erange else (2 + 2) + (4 + 4)
+        self.elems = nvar * nel
+        self.bytes_per_elem = per_pair / 2.0
+        self.slab_per_elem = 3
+        self.metric_key = "batch_c4_erange" if self._erange else "batch_c4"
+        self.dtype = "f32->i16/f32" if self._erange else "i16/f32"
+        self.kernel = ("k_batch<PutOp<NC_SHORT, float>> + k_batch<SwapOp<4>>" if self._erange
+                       else "k_batch_swapmix")
+        self.cfg = {"workload": ("C4 secondary: iput_vara batch, 128 NC_SHORT vars from float in [-40000, 40000] "
+                                 "(~18% NC_ERANGE + fill) + 128 NC_FLOAT vars, 2^20 elements each" if self._erange
+                                 else "C4: iput_vara batch, 256 variables x 2^20 elements, NC_SHORT/NC_FLOAT mixed"),
+                    "variables": nvar, "elements_per_var": nel,
+                    "call": "pncx_dev_batch_async (statuses in HBM)" if self._async
+                    else "pncx_dev_batch (statuses to host, synchronous)"}
+
+    def check(self):
+        T = self._T
+        exp = [T.NC_ERANGE if (self._erange and v % 2 == 0) else 0 for v in range(self._nvar)]
+        if self._async:
+            return self._tdst.cpu().tolist() == exp
+        return list(self._stv) == exp
+
+
+def _ok(rc, allowed=0):
+    assert rc == 0 or rc == allowed, rc
+
+
+def make_workload(name, torch, lib, sptr, args, world, rank):
+    if name == "c2":
+        return C2Swap(torch, lib, sptr, args.slab_gib, world, rank)
+    if name == "c3":
+        return C3IntDouble(torch, lib, sptr, rank)
+    if name == "c4":
+        return C4Batch(torch, lib, sptr, "async" if args.async_batch else "sync", rank)
+    if name == "c4_async":
+        return C4Batch(torch, lib, sptr, "async", rank)
+    if name == "c4_erange":
+        return C4Batch(torch, lib, sptr, "erange", rank)
+    raise ValueError(name)
+
+
+def measure(torch, lib, group, stream, wl, steps, warmup):
+    """W untimed warmups, then K steps between barrier + synchronize; HIP
+    events on the kernel's stream around every launch (for the synchronous
+    batch call the library's own events around its kernels).  Returns
+    (max-over-ranks wall seconds, kernel ms per launch, call ms or None)."""
+    torch.cuda.synchronize()
+    for _ in range(warmup):
+        wl.launch()
+    torch.cuda.synchronize()
+    if wl.lib_timed:
+        lib.pncx_dev_batch_timing(1)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    group.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        evs[k][0].record(stream)
+        wl.launch()
+        evs[k][1].record(stream)
+    torch.cuda.synchronize()
+    group.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / steps
+    call_ms = None
+    if wl.lib_timed:
+        tot, calls = ctypes.c_double(), ctypes.c_longlong()
+        assert lib.pncx_dev_batch_kernel_ms(ctypes.byref(tot), ctypes.byref(calls)) == 0 and calls.value == steps
+        call_ms, kern_ms = kern_ms, tot.value / calls.value
+        lib.pncx_dev_batch_timing(0)
+    elapsed, kern_ms = group.max([elapsed, kern_ms])
+    return elapsed, kern_ms, call_ms
+
+
+def summary(wl, elapsed, kern_ms, call_ms, steps, world):
+    moved = float(wl.bytes_per_elem) * wl.elems * world * steps
+    value = moved / elapsed / GIB
+    achieved = wl.bytes_per_elem * wl.elems / (kern_ms * 1e-3) / 1e9         # GB/s per GPU, per launch
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(wl.metric_key, wl.elems),
+            "kernel": wl.kernel, "kernel_ms_avg": round(kern_ms, 4),
+            "algorithmic_bytes_per_launch": int(wl.bytes_per_elem * wl.elems)}
+    if call_ms is not None:
+        roof["call_ms_avg"] = round(call_ms, 4)
+    return value, elapsed * 1e3 / steps, roof
+
+
+def worker(args):
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if os.environ.get("PNCX_DIST_BACKEND", "nccl") != "nccl":
+    backend = os.environ.get("PNCX_DIST_BACKEND", "nccl")      # nccl == RCCL on ROCm
+    if args.probe_launch:                                    # launcher check: no GPU work at all
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local, "gpus_arg": args.gpus}), flush=True)
+        return 0
+    if backend != "nccl":
         local = 0          # rehearsal: every rank on GPU 0
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = os.environ.get("PNCX_DIST_BACKEND", "nccl")   # nccl == RCCL on ROCm
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:   # rehearsal of the N>1 path with several ranks on one GPU
             dist.init_process_group(backend)
-    from pnetcdf_amd import nctypes as T
     from pnetcdf_amd import pncx
-    from pnetcdf_amd.shard import Group, record_slab
+    from pnetcdf_amd.shard import Group
     lib = pncx.lib()
-    group = Group(dist, torch.device("cuda", local) if os.environ.get("PNCX_DIST_BACKEND", "nccl") == "nccl"
-                  else "cpu")
+    group = Group(dist, torch.device("cuda", local) if backend == "nccl" else "cpu")
     stream = torch.cuda.current_stream()
     sptr = ctypes.c_void_p(stream.cuda_stream)
 
-    # ---------------------------------------------------------- workload
-    if args.workload == "c2":
-        n = int(args.slab_gib * GIB) // 8                      # NC_DOUBLE elements per rank
-        rec_elems = 8192 * 16384                               # one 1 GiB record of v(time, 8192, 16384)
-        nrec_total = (n // rec_elems) * world
-        first_rec, my_recs = record_slab(nrec_total, world, rank)
-        buf = torch.empty(n, dtype=torch.int64, device="cuda")
-        splitmix64_fill(torch, buf, SEEDS["c5" if world > 1 else "c2"] + first_rec)
-        ptr = ctypes.c_void_p(buf.data_ptr())
-        bytes_per_elem = 16                                    # 8 R + 8 W
-        slab_per_elem = 8                                      # external (file) bytes per element
-
-        def launch():
-            rc = lib.pncx_dev_in_swapn(ptr, n, 8, sptr)
-            assert rc == 0, rc
-        elems = n
-        metric_key = "swap8"
-        dtype = "u64"
-        recs = my_recs
-        cfg = {"workload": ("C2: 32 GiB contiguous NC_DOUBLE get_vara, in-place 8-byte swap" if world == 1 else
-                            f"C5: NC_DOUBLE record variable v(time={nrec_total}, 8192, 16384), "
-                            f"{recs} x 1 GiB records per GPU, in-place 8-byte swap"),
-               "slab_gib_per_gpu": args.slab_gib, "elements_per_gpu": n, "xtype": "NC_DOUBLE",
-               "itype": "double", "records_per_gpu": recs,
-               "parallelism": f"records sharded one slab per GPU x{world}, no data-path collective"}
-    elif args.workload == "c3":
-        n = 1 << 31                                            # NC_INT elements
-        xb = torch.empty(n // 2, dtype=torch.int64, device="cuda")
-        splitmix64_fill(torch, xb, SEEDS["c3"] + rank)
-        ib = torch.empty(n, dtype=torch.float64, device="cuda")
-        st = torch.zeros(1, dtype=torch.int32, device="cuda")
-        px, pi, ps = (ctypes.c_void_p(t.data_ptr()) for t in (xb, ib, st))
-
-        def launch():
-            rc = lib.pncx_dev_getn(5, T.NC_INT, px, pi, n, T.ITYPE_DOUBLE, ps, sptr)
-            assert rc == 0, rc
-        elems = n
-        bytes_per_elem = 12
-        slab_per_elem = 4
-        metric_key = "get_int_double"
-        dtype = "int32->f64"
-        cfg = {"workload": "C3: NC_INT on disk read via get_vara_double, fused 4-byte swap + int32->double",
-               "elements_per_gpu": n, "xtype": "NC_INT", "itype": "double", "parallelism": f"x{world}"}
-    else:
-        nvar, nel = 256, 1 << 20
-        segs = []
-        keep = []
-        for v in range(nvar):
-            if v % 2 == 0:
-                xt, it, isz = T.NC_SHORT, T.ITYPE_SHORT, 2
-            else:
-                xt, it, isz = T.NC_FLOAT, T.ITYPE_FLOAT, 4
-            ib = torch.randint(-2**31, 2**31 - 1, (nel * isz // 4,), dtype=torch.int32, device="cuda")
-            xb = torch.empty(nel * isz, dtype=torch.uint8, device="cuda")
-            keep += [ib, xb]
-            segs.append(pncx.Seg(T.PNCX_PUT, 5, xt, it, nel, xb.data_ptr(), ib.data_ptr(), None))
-        arr = (pncx.Seg * nvar)(*segs)
-        stv = (ctypes.c_int * nvar)()
-        dstv = torch.zeros(nvar, dtype=torch.int32, device="cuda")
-        dstp = ctypes.c_void_p(dstv.data_ptr())
-
-        def launch():
-            if args.async_batch:
-                rc = lib.pncx_dev_batch_async(arr, nvar, dstp, sptr)
-            else:
-                rc = lib.pncx_dev_batch(arr, nvar, stv, sptr)
-            assert rc == 0, rc
-        elems = nvar * nel
-        bytes_per_elem = 6                                     # avg of 2*2 (short) and 2*4 (float)
-        slab_per_elem = 3
-        metric_key = "batch_c4"
-        dtype = "i16/f32"
-        cfg = {"workload": "C4: iput_vara batch, 256 variables x 2^20 elements, NC_SHORT/NC_FLOAT mixed",
-               "variables": nvar, "elements_per_var": nel, "parallelism": f"x{world}",
-               "call": "pncx_dev_batch_async (statuses in HBM)" if args.async_batch
-               else "pncx_dev_batch (statuses to host, synchronous)"}
-
-    torch.cuda.synchronize()
-    for _ in range(args.warmup):
-        launch()
-    torch.cuda.synchronize()
-    if args.workload == "c4" and not args.async_batch:
-        # the batch call also copies the statuses back and waits: its kernel
-        # time comes from HIP events the library records around the launch
-        lib.pncx_dev_batch_timing(1)
-
-    # ---------------------------------------------------------- timed region
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    group.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        evs[k][0].record(stream)
-        launch()
-        evs[k][1].record(stream)
-    torch.cuda.synchronize()
-    group.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-    call_ms = None
-    if args.workload == "c4" and args.async_batch:
-        assert int(dstv.abs().sum().item()) == 0        # swaps: no segment may report NC_ERANGE
-    if args.workload == "c4" and not args.async_batch:
-        tot, calls = ctypes.c_double(), ctypes.c_longlong()
-        assert lib.pncx_dev_batch_kernel_ms(ctypes.byref(tot), ctypes.byref(calls)) == 0 and calls.value == args.steps
-        call_ms, kern_ms = kern_ms, tot.value / calls.value
-        lib.pncx_dev_batch_timing(0)
-    elapsed, kern_ms = group.max([elapsed, kern_ms])         # max over ranks
-
+    # ------------------------------------------------ headline (value)
+    head = "c4" if args.workload == "c4_async" else args.workload
+    if args.workload == "c4_async":
+        args.async_batch = True
+    wl = make_workload(args.workload if args.workload != "c4_async" else "c4", torch, lib, sptr, args, world, rank)
+    elapsed, kern_ms, call_ms = measure(torch, lib, group, stream, wl, args.steps, args.warmup)
+    ok = wl.check()
+    value, ms_per_step, roof = summary(wl, elapsed, kern_ms, call_ms, args.steps, world)
     gather = None
-    if world > 1 and args.gather_gib > 0 and args.workload == "c2":
-        gather = gather_leg(torch, group, buf, args.gather_gib,
-                            to_cpu=os.environ.get("PNCX_DIST_BACKEND", "nccl") != "nccl")
+    if world > 1 and args.gather_gib > 0 and head == "c2":
+        gib = args.gather_gib if backend == "nccl" else min(args.gather_gib, 1.0)   # gloo rehearsal: 1 GiB
+        gather = gather_leg(torch, group, wl._tbuf, gib, min(args.gather_chunk_gib, gib), to_cpu=backend != "nccl")
+    line = {
+        "metric": "GiB/s device-resident swap+type-convert, 2/4/8-byte NC arrays",
+        "value": round(value, 2),
+        "slab_GiBps": round(value * wl.slab_per_elem / wl.bytes_per_elem, 2),   # external bytes / t (SURVEY §8(d))
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": wl.dtype,
+        "data": "synthetic (splitmix64 bit patterns generated on the GPU)",
+        "config": wl.cfg,
+        "roofline": roof,
+        "check_ok": ok,
+    }
+    wl.free()
+    del wl
+    torch.cuda.empty_cache()
 
-    moved = float(bytes_per_elem) * elems * world * args.steps
-    value = moved / elapsed / GIB
-    ms_per_step = elapsed * 1e3 / args.steps
-    achieved = bytes_per_elem * elems / (kern_ms * 1e-3) / 1e9           # GB/s per GPU, per launch
-    traffic = load_traffic(metric_key, elems)
+    # ------------------------------------------------ the other 1-GPU configs
+    if world == 1 and not args.no_extra and head == "c2":
+        extra = {}
+        for name in EXTRA:
+            w = make_workload(name, torch, lib, sptr, args, world, rank)
+            el, km, cm = measure(torch, lib, group, stream, w, args.extra_steps, args.warmup)
+            v, mps, rf = summary(w, el, km, cm, args.extra_steps, world)
+            extra[name] = {"value": round(v, 2), "unit": "GiB/s", "ms_per_step": round(mps, 4),
+                           "steps": args.extra_steps, "dtype": w.dtype, "config": w.cfg, "roofline": rf,
+                           "check_ok": w.check()}
+            w.free()
+            del w
+            torch.cuda.empty_cache()
+        line["workloads"] = extra
 
     if rank == 0:
-        cpu = cpu_all = None
-        if world == 1 and not args.no_cpu_baseline and args.workload == "c2":
-            cpu = cpu_baseline_swap8(args.cpu_budget)
-            cpu_all = cpu_baseline_swap8_threads()
-        line = {
-            "metric": "GiB/s device-resident swap+type-convert, 2/4/8-byte NC arrays",
-            "value": round(value, 2),
-            "slab_GiBps": round(value * slab_per_elem / bytes_per_elem, 2),   # external bytes / t
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": dtype,
-            "data": "synthetic (splitmix64 bit patterns generated on the GPU)",
-            "config": cfg,
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
-                         "kernel_ms_avg": round(kern_ms, 4),
-                         **({"call_ms_avg": round(call_ms, 4)} if call_ms is not None else {}),
-                         "algorithmic_bytes_per_launch": bytes_per_elem * elems},
-            "cpu_baseline": cpu,
-            "cpu_baseline_all_cores": cpu_all,
-        }
+        if world == 1 and not args.no_cpu_baseline and head == "c2":
+            line["cpu_baseline"] = cpu_baseline_swap8(args.cpu_budget)
+            line["cpu_baseline_all_cores"] = cpu_baseline_swap8_threads()
+            if "workloads" in line:
+                from pnetcdf_amd import nctypes as T
+                line["workloads"]["c3"]["cpu_baseline"] = cpu_baseline_getn(T.NC_INT, T.ITYPE_DOUBLE, 4, 8,
+                                                                            seed=SEEDS["c3"])
+        else:
+            line["cpu_baseline"] = None
         if gather is not None:
             line["gather"] = gather
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    return 0
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c4_async", "c4_erange"])
+    ap.add_argument("--slab-gib", type=float, default=32.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="N=1, c2: skip the c3/c4 workloads")
+    ap.add_argument("--extra-steps", type=int, default=20)
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--async-batch", action="store_true",
+                    help="c4: pncx_dev_batch_async (statuses stay in HBM, calls queue back to back) "
+                         "instead of the synchronous pncx_dev_batch")
+    ap.add_argument("--gather-gib", type=float, default=32.0,
+                    help="N>1, c2: GiB per rank gathered into rank 0 after the timed region (0 = off)")
+    ap.add_argument("--gather-chunk-gib", type=float, default=2.0)
+    ap.add_argument("--probe-launch", action="store_true", help=argparse.SUPPRESS)
+    args = ap.parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus > 1:
+            return launch_ranks(args.gpus, argv)
+    elif int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}; refusing to report a mislabelled run",
+              file=sys.stderr)
+        return 2
+    return worker(args)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -292,6 +292,9 @@ typedef struct ctx_t {
     void  *async_stream;      /* stream of the last async upload not yet known complete */
     int    async_pending;
     struct pncx_seg *cache_segs;
+    uint64_t *cache_fills;    /* the bytes *fillp held when the plan was made: the
+                               * plan carries the fill value (classify), the
+                               * segment array only its address */
     struct cls_t *cache_cls;
     size_t cache_soff, cache_moff;
     void  *ev;                /* completion event for the spin-wait */
@@ -1389,6 +1392,24 @@ static int spin_wait(ctx_t *c, void *stream)
     return pncxrt_event_sync(c->ev);
 }
 
+/* the fill value a put segment's plan was classified with (classify copies
+ * xlen bytes of *fillp into the op), zero-extended; 0 for gets and NULL fills */
+static uint64_t fill_word(const pncx_seg *s)
+{
+    uint64_t w = 0;
+    const int xs = pncx_xlen(s->xtype);
+    if (s->dir == PNCX_PUT && s->fillp != NULL && xs > 0 && xs <= 8) memcpy(&w, s->fillp, (size_t)xs);
+    return w;
+}
+
+static int same_fills(const uint64_t *cached, const pncx_seg *segs, int nseg)
+{
+    int i;
+    for (i = 0; i < nseg; i++)
+        if (cached[i] != fill_word(&segs[i])) return 0;
+    return 1;
+}
+
 /* dstatus == NULL: synchronous pncx_dev_batch (statuses come back to the
  * host, epoch values in the scratch status words); else pncx_dev_batch_async
  * (the kernels set the caller's device words to NC_ERANGE; nothing waits) */
@@ -1411,7 +1432,8 @@ static int dev_batch(const pncx_seg *segs, int nseg, int *status_out, int *dstat
     if (c->epoch == 0) { c->epoch = 1; c->cache_valid = 0; }
     sval = async ? NC_ERANGE : 0x40000000 | c->epoch;
     if (c->cache_valid && c->cache_nseg == nseg && c->cache_dstatus == dstatus &&
-        memcmp(c->cache_segs, segs, sizeof(pncx_seg) * (size_t)nseg) == 0) {
+        memcmp(c->cache_segs, segs, sizeof(pncx_seg) * (size_t)nseg) == 0 &&
+        same_fills(c->cache_fills, segs, nseg)) {
         /* async calls on a cached plan read the device descriptors until they
          * finish: the next re-plan waits for their stream, so only one stream
          * may have such calls outstanding -- switching streams drains the old one */
@@ -1491,10 +1513,13 @@ static int dev_batch(const pncx_seg *segs, int nseg, int *status_out, int *dstat
         if (!err && unbatched == 0 && nclassified == nseg) {
             pncx_seg *cs = (pncx_seg *)realloc(c->cache_segs, sizeof(pncx_seg) * (size_t)nseg);
             cls_t *cc = (cls_t *)realloc(c->cache_cls, sizeof(cls_t) * (size_t)(plan.ncls ? plan.ncls : 1));
+            uint64_t *cf = (uint64_t *)realloc(c->cache_fills, sizeof(uint64_t) * (size_t)nseg);
             if (cs) c->cache_segs = cs;
             if (cc) c->cache_cls = cc;
-            if (cs && cc) {
+            if (cf) c->cache_fills = cf;
+            if (cs && cc && cf) {
                 memcpy(cs, segs, sizeof(pncx_seg) * (size_t)nseg);
+                for (i = 0; i < nseg; i++) cf[i] = fill_word(&segs[i]);
                 memcpy(cc, plan.cls, sizeof(cls_t) * (size_t)plan.ncls);
                 c->cache_nseg = nseg;
                 c->cache_ncls = plan.ncls;

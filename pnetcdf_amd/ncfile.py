@@ -391,8 +391,17 @@ def get_var_dev(ncid, varid, t, start=None, count=None, stride=None, imap=None, 
                                       ctypes.c_void_p(s.cuda_stream))
 
 
+def _nb_contig(buf):
+    """A nonblocking request keeps the raw pointer until wait: a strided view
+    would be read or written as if packed, and a contiguous copy would die
+    before the wait, so the caller must pass a C-contiguous array."""
+    if not buf.flags["C_CONTIGUOUS"]:
+        raise ValueError("nonblocking requests need a C-contiguous buffer that lives until wait")
+
+
 def iput_var(ncid, varid, buf, start=None, count=None, stride=None, imap=None, itype=None):
     """ncmpi_iput_var*: the buffer must stay alive and unchanged until wait"""
+    _nb_contig(buf)
     keep, a = _args(start, count, stride, imap)
     it = itype if itype is not None else itype_of(buf)
     r = ctypes.c_int(NC_REQ_NULL)
@@ -401,6 +410,7 @@ def iput_var(ncid, varid, buf, start=None, count=None, stride=None, imap=None, i
 
 
 def iget_var(ncid, varid, out, start=None, count=None, stride=None, imap=None, itype=None):
+    _nb_contig(out)
     keep, a = _args(start, count, stride, imap)
     it = itype if itype is not None else itype_of(out)
     r = ctypes.c_int(NC_REQ_NULL)
@@ -479,6 +489,7 @@ def put_varn(ncid, varid, starts, counts, buf, itype=None):
 
 
 def get_varn(ncid, varid, starts, counts, out, itype=None):
+    assert out.flags["C_CONTIGUOUS"]
     ks, ps = _ptr_array(starts)
     kc, pc = _ptr_array(counts)
     it = itype if itype is not None else itype_of(out)
@@ -487,6 +498,7 @@ def get_varn(ncid, varid, starts, counts, out, itype=None):
 
 
 def iput_varn(ncid, varid, starts, counts, buf, itype=None):
+    _nb_contig(buf)
     ks, ps = _ptr_array(starts)
     kc, pc = _ptr_array(counts)
     it = itype if itype is not None else itype_of(buf)
@@ -497,6 +509,7 @@ def iput_varn(ncid, varid, starts, counts, buf, itype=None):
 
 
 def iget_varn(ncid, varid, starts, counts, out, itype=None):
+    _nb_contig(out)
     ks, ps = _ptr_array(starts)
     kc, pc = _ptr_array(counts)
     it = itype if itype is not None else itype_of(out)

@@ -215,6 +215,84 @@ def test_fill_mode_and_fill_var_rec(gpu, tmp_path):
     assert N.close(ncid) == 0
 
 
+def test_wait_all_fill_change_after_redef(gpu, tmp_path):
+    """iput -> wait_all -> redef + def_var_fill -> iput -> wait_all: the
+    second flush's ERANGE elements carry the new _FillValue even though the
+    request list (and its arena addresses) repeat, so the batch plan cache
+    must not reuse the first fill.  File bytes against
+    the oracle's putn with each fill (ncmpio_util.c:705-711 takes the fill
+    from ncmpio_inq_var_fill per request)."""
+    nel = 8192
+    p = str(tmp_path / "fillchg.nc")
+    err, ncid = N.create(p, N.NC_64BIT_DATA)
+    N.def_dim(ncid, "x", nel)
+    N.def_var(ncid, "s", T.NC_SHORT, [0])
+    N.def_var(ncid, "f", T.NC_FLOAT, [0])
+    assert N.enddef(ncid) == 0
+    rng = np.random.default_rng(5)
+    bs = rng.uniform(-40000, 40000, nel).astype(np.float32)     # ~18% ERANGE into NC_SHORT
+    bf = rng.standard_normal(nel).astype(np.float32)
+    ora = OracleConv()
+    for k, fv in enumerate((None, -555, 1234)):
+        if fv is not None:
+            assert N.redef(ncid) == 0
+            assert N.def_var_fill(ncid, 0, 0, np.array([fv], np.int16)) == 0
+            assert N.enddef(ncid) == 0
+        reqs = [N.iput_var(ncid, 0, bs, [0], [nel])[1], N.iput_var(ncid, 1, bf, [0], [nel])[1]]
+        err, st = N.wait_all(ncid, reqs)
+        assert err == N.NC_ERANGE and st == [N.NC_ERANGE, 0]
+        assert N.sync(ncid) == 0
+        raw = _raw(p)
+        h = cdfparse.parse_cdf(raw)
+        fill = T.fill_bytes(T.NC_SHORT, fv)
+        exp, so = ora.putn(5, T.NC_SHORT, bs, T.ITYPE_FLOAT, fill)
+        assert so == T.NC_ERANGE
+        assert _var_bytes(raw, h, "s", None, nel * 2) == exp, (k, fv)
+    assert N.close(ncid) == 0
+
+
+def test_pending_requests_across_redef(gpu, tmp_path):
+    """ncmpio_redef (ncmpio_file_misc.c:80-108) accepts pending nonblocking
+    requests.  iput + iget posted, redef adds a variable and a header-growing
+    attribute, enddef moves the data, then wait_all: the put lands at the
+    variable's new offset, the get reads the moved data, and the put's
+    ERANGE elements carry the fill of POST time (the reference converts an
+    iput when it is posted, ncmpio_i_getput.m4:300-303), not the
+    _FillValue defined in between."""
+    nel = 4096
+    p = str(tmp_path / "pend.nc")
+    err, ncid = N.create(p, N.NC_64BIT_DATA)
+    N.def_dim(ncid, "x", nel)
+    N.def_var(ncid, "a", T.NC_SHORT, [0])
+    N.def_var(ncid, "b", T.NC_INT, [0])
+    assert N.enddef(ncid) == 0
+    rng = np.random.default_rng(9)
+    vb = rng.integers(-2**31, 2**31 - 1, nel, dtype=np.int32)
+    assert N.put_var(ncid, 1, vb) == 0
+    off_a0 = N.inq_varoffset(ncid, 0)[1]
+    va = rng.uniform(-40000, 40000, nel).astype(np.float64)
+    got = np.zeros(nel, np.int64)
+    err, rp = N.iput_var(ncid, 0, va, [0], [nel])
+    assert err == 0
+    err, rg = N.iget_var(ncid, 1, got, [0], [nel])
+    assert err == 0
+    assert N.redef(ncid) == 0
+    assert N.put_att_text(ncid, N.NC_GLOBAL, "pad", "z" * 3000) == 0
+    N.def_var(ncid, "c", T.NC_DOUBLE, [0])
+    assert N.def_var_fill(ncid, 0, 0, np.array([-77], np.int16)) == 0
+    assert N.enddef(ncid) == 0
+    assert N.inq_varoffset(ncid, 0)[1] > off_a0                # the data moved
+    err, st = N.wait_all(ncid, [rp, rg])
+    assert err == N.NC_ERANGE and st == [N.NC_ERANGE, 0]
+    assert np.array_equal(got, vb.astype(np.int64))
+    assert N.close(ncid) == 0
+    raw = _raw(p)
+    h = cdfparse.parse_cdf(raw)
+    exp, _ = OracleConv().putn(5, T.NC_SHORT, va, T.ITYPE_DOUBLE, T.fill_bytes(T.NC_SHORT))
+    assert _var_bytes(raw, h, "a", None, nel * 2) == exp
+    assert _var_bytes(raw, h, "b", None, nel * 4) == vb.astype(">i4").tobytes()
+
+
 def test_nonblocking_c4_batch(gpu, tmp_path):
     """config-4 shape: many iput_vara of mixed NC_SHORT / NC_FLOAT flushed by
     one wait_all (one batched conversion); statuses per request, NC_ERANGE

@@ -1,0 +1,65 @@
+"""Where does the time of a float -> NC_SHORT put with out-of-range values
+go?  k_tile (pncx_dev_putn) and k_batch (pncx_dev_batch, 128 x 2^20) on
+three inputs: random bits, uniform [-40000, 40000] (~18% NC_ERANGE) and
+uniform [-30000, 30000] (none).  HIP events, ms per launch, GB/s."""
+import ctypes
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+    from pnetcdf_amd import nctypes as T
+    from pnetcdf_amd import pncx
+    lib = pncx.lib()
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    nseg, nel = 128, 1 << 20
+    n = nseg * nel
+    src = torch.empty(n, dtype=torch.float32, device="cuda")
+    dst = torch.empty(n * 2, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    fb = (ctypes.c_uint8 * 16)(0x01, 0x80)
+    fp = ctypes.cast(fb, ctypes.c_void_p)
+    segs = (pncx.Seg * nseg)(*[pncx.Seg(T.PNCX_PUT, 5, T.NC_SHORT, T.ITYPE_FLOAT, nel, dst.data_ptr() + 2 * nel * k,
+                                        src.data_ptr() + 4 * nel * k, fp.value) for k in range(nseg)])
+    stv = (ctypes.c_int * nseg)()
+    dstat = torch.zeros(nseg, dtype=torch.int32, device="cuda")
+    out = []
+    for name in ("bits", "u40000", "u30000", "u40000_sorted"):
+        if name == "bits":
+            src.view(torch.int32).random_()
+        elif name.startswith("u40000"):
+            src.uniform_(-40000, 40000)
+            if name.endswith("sorted"):
+                src.copy_(src.sort().values)
+        else:
+            src.uniform_(-30000, 30000)
+        for kind in ("tile", "batch", "batch_async"):
+            def run():
+                if kind == "tile":
+                    rc = lib.pncx_dev_putn(5, T.NC_SHORT, ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()),
+                                           n, T.ITYPE_FLOAT, fp, ctypes.c_void_p(st.data_ptr()), sp)
+                elif kind == "batch":
+                    rc = lib.pncx_dev_batch(segs, nseg, stv, sp)
+                else:
+                    rc = lib.pncx_dev_batch_async(segs, nseg, ctypes.c_void_p(dstat.data_ptr()), sp)
+                assert rc in (0, T.NC_ERANGE), rc
+            for _ in range(3):
+                run()
+            torch.cuda.synchronize()
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+            for a, b in ev:
+                a.record()
+                run()
+                b.record()
+            torch.cuda.synchronize()
+            ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+            out.append({"input": name, "kernel": kind, "ms": round(ms, 4), "GBps": round(6 * n / ms / 1e6, 1)})
+            print(json.dumps(out[-1]), flush=True)
+
+
+if __name__ == "__main__":
+    main()
