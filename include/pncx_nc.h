@@ -133,6 +133,19 @@ int pncx_nc_close(int ncid);
  * the application reduces numrecs (max) and rank 0 records it here before
  * close (ncmpio_write_numrecs, ncmpio_util.c). */
 int pncx_nc_sync_numrecs(int ncid, pncx_offset numrecs);
+/* One file shared by several processes (the ncmpi_* driver on a
+ * communicator, one process per GPU).  Every process keeps its own copy of
+ * the header and runs the same define-mode calls; only the writer (rank 0)
+ * writes header bytes and numrecs, moves data at enddef and fills new
+ * variables, as the reference writes them from the root
+ * (ncmpio_enddef.c:681, ncmpio_sync.c).  The caller orders the processes:
+ * the writer creates (truncates) the file before the others open it with
+ * pncx_nc_create_shared(writer = 0), and enddef/close are followed by a
+ * barrier.  pncx_nc_set_numrecs raises this handle's numrecs (the MAX of
+ * ncmpio_getput.m4:289-311) without writing it. */
+int pncx_nc_create_shared(const char *path, int cmode, int writer, int *ncid);
+int pncx_nc_set_writer(int ncid, int writer);
+int pncx_nc_set_numrecs(int ncid, pncx_offset numrecs);
 
 /* ---- define mode ---- */
 int pncx_nc_def_dim(int ncid, const char *name, pncx_offset len, int *dimid);
@@ -215,6 +228,8 @@ int pncx_nc_inq_buffer_usage(int ncid, pncx_offset *usage);
 int pncx_nc_bput_varm(int ncid, int varid, const pncx_offset *start, const pncx_offset *count,
                       const pncx_offset *stride, const pncx_offset *imap, const void *buf,
                       int itype, int *reqid);
+int pncx_nc_bput_varn(int ncid, int varid, int num, const pncx_offset *const *starts,
+                      const pncx_offset *const *counts, const void *buf, int itype, int *reqid);
 /* flexible API (ncmpi_{put,get,iput,iget}_varm[_all] with bufcount + an MPI
  * derived buftype, dispatchers/var_getput.m4:312-382, ncmpio_getput.m4:136-
  * 235): the user buffer is `bufcount` copies of a committed flattened

@@ -1,0 +1,381 @@
+/*
+ * api_check.c -- programs written against the public ncmpi_* API
+ * (include/pnetcdf.h) and linked with libpnetcdf.so, in the shape of the
+ * reference's benchmarks and tests.  Test infrastructure: tests/
+ * test_gpu_c_api.py and tests/test_c_api_cpu.py run the modes and check
+ * the files they write against the CPU oracle.
+ *
+ *   api_check c1 <nc> <in.bin> <n>
+ *       BASELINE config 1 (benchmarks/C pattern, 1 rank): 1-D NC_INT x(n),
+ *       ncmpi_put_vara_int_all of in.bin, close, reopen,
+ *       ncmpi_get_vara_int_all (must equal the input) and
+ *       ncmpi_get_vara_double_all (config 3's read: must equal (double)).
+ *   api_check putvara <nc> <nvars> <len> <ntimes> <nonblocking> [indep]
+ *       benchmarks/C/pnetcdf_put_vara.c:138-219 on 1..N ranks: record
+ *       variables float var_i(time, Y, X), text/float/short attributes,
+ *       ncmpi_iput_vara_float x nvars x ntimes + ncmpi_wait_all (or
+ *       ncmpi_put_vara_float[_all]); each rank a 2-D block.
+ *   api_check c4 <nc> <shorts.bin> <floats.bin> <nel> <erange>
+ *       BASELINE config 4: 256 variables, ncmpi_iput_vara_short/float x 256
+ *       + one ncmpi_wait_all; erange = 1 is §8(d)'s secondary variant (the
+ *       NC_SHORT variables written from float with NC_ERANGE).
+ *   api_check records <nc> <nrec> <x>
+ *       config 5 at file level on N ranks: a record variable
+ *       v(time, x) NC_DOUBLE, rank r writes its slab of records with
+ *       ncmpi_put_vara_double_all; reopened, every rank reads every record.
+ *   api_check errors <dir>
+ *       argument and mode errors the dispatcher returns before any
+ *       conversion (no GPU needed): prints "name code" lines.
+ *   api_check header <nc> [nranks-agnostic]
+ *       define-mode only (dims, variables, text attributes) on N ranks: the
+ *       header rank 0 writes must not depend on N.
+ */
+#include <mpi.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "pnetcdf.h"
+
+static int nerrs = 0;
+#define CHECK(call)                                                                                  \
+    do {                                                                                             \
+        int _e = (call);                                                                             \
+        if (_e != NC_NOERR) {                                                                        \
+            fprintf(stderr, "%s:%d: %s -> %d %s\n", __FILE__, __LINE__, #call, _e, ncmpi_strerror(_e)); \
+            nerrs++;                                                                                 \
+        }                                                                                            \
+    } while (0)
+
+static void *slurp(const char *path, size_t *len)
+{
+    FILE *f = fopen(path, "rb");
+    void *b;
+    if (f == NULL) return NULL;
+    fseek(f, 0, SEEK_END);
+    *len = (size_t)ftell(f);
+    fseek(f, 0, SEEK_SET);
+    b = malloc(*len + 1);
+    if (b && fread(b, 1, *len, f) != *len) { free(b); b = NULL; }
+    fclose(f);
+    return b;
+}
+
+static int mode_c1(const char *path, const char *inpath, MPI_Offset n)
+{
+    size_t len;
+    int *in = (int *)slurp(inpath, &len), *got, ncid, dimid, varid, i;
+    double *gd;
+    MPI_Offset start[1] = {0}, count[1] = {n}, put = 0, get = 0;
+    if (in == NULL || len != (size_t)n * 4) { fprintf(stderr, "bad input\n"); return 1; }
+    CHECK(ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid));
+    CHECK(ncmpi_def_dim(ncid, "x", n, &dimid));
+    CHECK(ncmpi_def_var(ncid, "v", NC_INT, 1, &dimid, &varid));
+    CHECK(ncmpi_enddef(ncid));
+    CHECK(ncmpi_put_vara_int_all(ncid, varid, start, count, in));
+    CHECK(ncmpi_inq_put_size(ncid, &put));
+    CHECK(ncmpi_close(ncid));
+    got = (int *)calloc((size_t)n, sizeof(int));
+    gd = (double *)calloc((size_t)n, sizeof(double));
+    CHECK(ncmpi_open(MPI_COMM_WORLD, path, NC_NOWRITE, MPI_INFO_NULL, &ncid));
+    CHECK(ncmpi_inq_varid(ncid, "v", &varid));
+    CHECK(ncmpi_get_vara_int_all(ncid, varid, start, count, got));
+    CHECK(ncmpi_get_vara_double_all(ncid, varid, start, count, gd));
+    CHECK(ncmpi_inq_get_size(ncid, &get));
+    CHECK(ncmpi_close(ncid));
+    for (i = 0; i < n; i++) {
+        if (got[i] != in[i]) { fprintf(stderr, "int mismatch at %d\n", i); nerrs++; break; }
+        if (gd[i] != (double)in[i]) { fprintf(stderr, "double mismatch at %d\n", i); nerrs++; break; }
+    }
+    printf("{\"mode\": \"c1\", \"n\": %lld, \"put_size\": %lld, \"get_size\": %lld, \"errors\": %d}\n",
+           (long long)n, (long long)put, (long long)get, nerrs);
+    free(in);
+    free(got);
+    free(gd);
+    return nerrs != 0;
+}
+
+/* benchmarks/C/pnetcdf_put_vara.c:90-219 restated as a check */
+static int mode_putvara(const char *path, int nvars, int len, int ntimes, int nonblocking, int indep)
+{
+    int i, j, rank, nprocs, psizes[2] = {0, 0}, ncid, *varid, dimid[3];
+    float **buf;
+    MPI_Offset start[3], count[3];
+    double t0, t1, tmax;
+    char name[64], str_att[128];
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    MPI_Comm_size(MPI_COMM_WORLD, &nprocs);
+    MPI_Dims_create(nprocs, 2, psizes);
+    buf = (float **)malloc(sizeof(float *) * (size_t)nvars);
+    varid = (int *)malloc(sizeof(int) * (size_t)nvars);
+    for (i = 0; i < nvars; i++) {
+        buf[i] = (float *)malloc(sizeof(float) * (size_t)len * (size_t)len);
+        for (j = 0; j < len * len; j++) buf[i][j] = (float)(rank + i * len + j);
+    }
+    MPI_Barrier(MPI_COMM_WORLD);
+    t0 = MPI_Wtime();
+    CHECK(ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid));
+    snprintf(str_att, sizeof str_att, "Thu Aug 29 14:29:35 2024");
+    CHECK(ncmpi_put_att_text(ncid, NC_GLOBAL, "history", (MPI_Offset)strlen(str_att), str_att));
+    CHECK(ncmpi_def_dim(ncid, "time", NC_UNLIMITED, &dimid[0]));
+    CHECK(ncmpi_def_dim(ncid, "Y", (MPI_Offset)psizes[0] * len, &dimid[1]));
+    CHECK(ncmpi_def_dim(ncid, "X", (MPI_Offset)psizes[1] * len, &dimid[2]));
+    for (i = 0; i < nvars; i++) {
+        short short_att = 1234;
+        float float_att[4] = {0, 1, 2, 3};
+        snprintf(name, sizeof name, "var_%d", i);
+        CHECK(ncmpi_def_var(ncid, name, NC_FLOAT, 3, dimid, &varid[i]));
+        snprintf(str_att, sizeof str_att, "some text attribute %d type text.", i);
+        CHECK(ncmpi_put_att_text(ncid, varid[i], "str_att", (MPI_Offset)strlen(str_att), str_att));
+        CHECK(ncmpi_put_att_float(ncid, varid[i], "float_att", NC_FLOAT, 4, float_att));
+        CHECK(ncmpi_put_att_short(ncid, varid[i], "short_att", NC_SHORT, 1, &short_att));
+    }
+    CHECK(ncmpi_enddef(ncid));
+    if (indep) CHECK(ncmpi_begin_indep_data(ncid));
+    start[1] = (MPI_Offset)len * (rank / psizes[1]);
+    start[2] = (MPI_Offset)len * (rank % psizes[1]);
+    count[0] = 1;
+    count[1] = len;
+    count[2] = len;
+    t1 = MPI_Wtime();
+    for (j = 0; j < ntimes; j++) {
+        start[0] = j;
+        for (i = 0; i < nvars; i++) {
+            if (nonblocking) CHECK(ncmpi_iput_vara_float(ncid, varid[i], start, count, buf[i], NULL));
+            else if (indep) CHECK(ncmpi_put_vara_float(ncid, varid[i], start, count, buf[i]));
+            else CHECK(ncmpi_put_vara_float_all(ncid, varid[i], start, count, buf[i]));
+        }
+    }
+    if (nonblocking) {
+        if (indep) CHECK(ncmpi_wait(ncid, NC_REQ_ALL, NULL, NULL));
+        else CHECK(ncmpi_wait_all(ncid, NC_REQ_ALL, NULL, NULL));
+    }
+    t1 = MPI_Wtime() - t1;
+    if (indep) CHECK(ncmpi_end_indep_data(ncid));
+    CHECK(ncmpi_close(ncid));
+    t0 = MPI_Wtime() - t0;
+    MPI_Reduce(&t1, &tmax, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
+    MPI_Allreduce(MPI_IN_PLACE, &nerrs, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);
+    if (rank == 0) {
+        const double w = 4.0 * nprocs * (double)len * len * nvars * ntimes;
+        printf("{\"mode\": \"putvara\", \"nprocs\": %d, \"py\": %d, \"px\": %d, \"bytes\": %.0f, "
+               "\"write_s\": %.6f, \"MiBps\": %.2f, \"errors\": %d}\n",
+               nprocs, psizes[0], psizes[1], w, tmax, w / 1048576.0 / tmax, nerrs);
+    }
+    for (i = 0; i < nvars; i++) free(buf[i]);
+    free(buf);
+    free(varid);
+    return nerrs != 0;
+}
+
+static int mode_c4(const char *path, const char *sp, const char *fp, MPI_Offset nel, int erange)
+{
+    const int nvar = 256;
+    size_t ls, lf;
+    short *sh = (short *)slurp(sp, &ls);
+    float *fl = (float *)slurp(fp, &lf);
+    int ncid, dimid, v, varid[256], reqs[256], st[256], err;
+    MPI_Offset start[1] = {0}, count[1] = {nel};
+    if (sh == NULL || fl == NULL || ls != (size_t)(nvar / 2) * nel * 2 || lf != (size_t)(nvar / 2) * nel * 4) {
+        fprintf(stderr, "bad input\n");
+        return 1;
+    }
+    CHECK(ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid));
+    CHECK(ncmpi_def_dim(ncid, "x", nel, &dimid));
+    for (v = 0; v < nvar; v++) {
+        char name[32];
+        snprintf(name, sizeof name, "v%d", v);
+        CHECK(ncmpi_def_var(ncid, name, v % 2 == 0 ? NC_SHORT : NC_FLOAT, 1, &dimid, &varid[v]));
+    }
+    CHECK(ncmpi_enddef(ncid));
+    for (v = 0; v < nvar; v++) {
+        const MPI_Offset k = v / 2;
+        if (v % 2 == 0 && !erange) CHECK(ncmpi_iput_vara_short(ncid, varid[v], start, count, sh + k * nel, &reqs[v]));
+        else CHECK(ncmpi_iput_vara_float(ncid, varid[v], start, count, fl + k * nel, &reqs[v]));
+    }
+    err = ncmpi_wait_all(ncid, nvar, reqs, st);
+    CHECK(ncmpi_close(ncid));
+    printf("{\"mode\": \"c4\", \"wait\": %d, \"statuses\": [", err);
+    for (v = 0; v < nvar; v++) printf("%s%d", v ? ", " : "", st[v]);
+    printf("], \"reqs_after\": %d, \"errors\": %d}\n", reqs[0], nerrs);
+    free(sh);
+    free(fl);
+    return nerrs != 0;
+}
+
+static int mode_records(const char *path, MPI_Offset nrec, MPI_Offset x)
+{
+    int rank, nprocs, ncid, dimid[2], varid, bad = 0;
+    MPI_Offset first, cnt, r, k, start[2], count[2], numrecs = -1;
+    double *b;
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    MPI_Comm_size(MPI_COMM_WORLD, &nprocs);
+    /* balanced contiguous slabs, the LAST records on rank 0 so that rank 0
+     * (the numrecs writer) never holds the largest record index alone */
+    {
+        const int slot = nprocs - 1 - rank;
+        const MPI_Offset base = nrec / nprocs, rem = nrec % nprocs;
+        first = slot * base + (slot < rem ? slot : rem);
+        cnt = base + (slot < rem ? 1 : 0);
+    }
+    b = (double *)malloc(sizeof(double) * (size_t)(nrec * x + 1));
+    for (r = first; r < first + cnt; r++)
+        for (k = 0; k < x; k++) b[(r - first) * x + k] = (double)r * 1000.0 + (double)k + 0.25;
+    CHECK(ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid));
+    CHECK(ncmpi_def_dim(ncid, "time", NC_UNLIMITED, &dimid[0]));
+    CHECK(ncmpi_def_dim(ncid, "x", x, &dimid[1]));
+    CHECK(ncmpi_def_var(ncid, "v", NC_DOUBLE, 2, dimid, &varid));
+    CHECK(ncmpi_enddef(ncid));
+    start[0] = first;
+    start[1] = 0;
+    count[0] = cnt;
+    count[1] = x;
+    CHECK(ncmpi_put_vara_double_all(ncid, varid, start, count, b));
+    CHECK(ncmpi_inq_dimlen(ncid, dimid[0], &numrecs));      /* MAX-synced after the collective put */
+    if (numrecs != nrec) { fprintf(stderr, "rank %d numrecs %lld after put\n", rank, (long long)numrecs); nerrs++; }
+    CHECK(ncmpi_close(ncid));
+    CHECK(ncmpi_open(MPI_COMM_WORLD, path, NC_NOWRITE, MPI_INFO_NULL, &ncid));
+    CHECK(ncmpi_inq_dimlen(ncid, 0, &numrecs));
+    if (numrecs != nrec) { fprintf(stderr, "rank %d numrecs %lld on disk\n", rank, (long long)numrecs); nerrs++; }
+    start[0] = 0;
+    count[0] = nrec;
+    CHECK(ncmpi_get_vara_double_all(ncid, 0, start, count, b));
+    for (r = 0; r < nrec && !bad; r++)
+        for (k = 0; k < x; k++)
+            if (b[r * x + k] != (double)r * 1000.0 + (double)k + 0.25) { bad = 1; break; }
+    if (bad) { fprintf(stderr, "rank %d data mismatch\n", rank); nerrs++; }
+    CHECK(ncmpi_close(ncid));
+    MPI_Allreduce(MPI_IN_PLACE, &nerrs, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);
+    if (rank == 0) printf("{\"mode\": \"records\", \"nprocs\": %d, \"nrec\": %lld, \"errors\": %d}\n", nprocs,
+                          (long long)nrec, nerrs);
+    free(b);
+    return nerrs != 0;
+}
+
+/* errors the dispatcher returns before any conversion (var_getput.m4
+ * sanity_check / check_start_count_stride, file.c, attr_getput.m4) */
+static int mode_errors(const char *dir)
+{
+    char path[512];
+    int ncid, dimid[2], v, vt, vr, e, i4[4] = {0}, req;
+    MPI_Offset st[2] = {0, 0}, ct[2] = {1, 1}, big[2] = {5, 0}, neg[2] = {-1, 1}, st1[2] = {1, 0}, sd0[2] = {0, 0};
+    float f = 1.0f;
+    snprintf(path, sizeof path, "%s/errors.nc", dir);
+#define R(name, call) printf("%s %d\n", name, (call))
+    R("create_bad_path", ncmpi_create(MPI_COMM_WORLD, "", NC_CLOBBER, MPI_INFO_NULL, &ncid));
+    R("create_both_formats", ncmpi_create(MPI_COMM_WORLD, path, NC_64BIT_DATA | NC_64BIT_OFFSET, MPI_INFO_NULL, &ncid));
+    R("create_netcdf4", ncmpi_create(MPI_COMM_WORLD, path, NC_NETCDF4, MPI_INFO_NULL, &ncid));
+    e = ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER, MPI_INFO_NULL, &ncid);
+    R("create", e);
+    R("noclobber_exists", ncmpi_create(MPI_COMM_WORLD, path, NC_NOCLOBBER, MPI_INFO_NULL, &v));
+    R("def_dim", ncmpi_def_dim(ncid, "t", NC_UNLIMITED, &dimid[0]));
+    R("def_dim_x", ncmpi_def_dim(ncid, "x", 4, &dimid[1]));
+    R("def_dim_second_unlimited", ncmpi_def_dim(ncid, "u2", NC_UNLIMITED, &v));
+    R("def_dim_name_in_use", ncmpi_def_dim(ncid, "x", 4, &v));
+    R("def_var_cdf1_int64", ncmpi_def_var(ncid, "w", NC_INT64, 1, &dimid[1], &v));
+    R("def_var_badtype", ncmpi_def_var(ncid, "w", 99, 1, &dimid[1], &v));
+    R("def_var", ncmpi_def_var(ncid, "v", NC_INT, 1, &dimid[1], &v));
+    R("def_var_text", ncmpi_def_var(ncid, "c", NC_CHAR, 1, &dimid[1], &vt));
+    R("def_var_rec", ncmpi_def_var(ncid, "r", NC_FLOAT, 2, dimid, &vr));
+    R("put_in_define_mode", ncmpi_put_vara_int_all(ncid, v, st, ct, i4));
+    R("inq_bad_ncid", ncmpi_inq(12345, NULL, NULL, NULL, NULL));
+    R("put_att_echar", ncmpi_put_att_int(ncid, NC_GLOBAL, "a", NC_CHAR, 1, i4));
+    R("put_att_strict_cdf2", ncmpi_put_att_int(ncid, NC_GLOBAL, "a", NC_UINT, 1, i4));
+    R("put_att_negative_len", ncmpi_put_att_text(ncid, NC_GLOBAL, "a", -1, "x"));
+    R("put_att_text", ncmpi_put_att_text(ncid, NC_GLOBAL, "title", 5, "hello"));
+    R("inq_att_missing", ncmpi_inq_att(ncid, NC_GLOBAL, "nope", NULL, NULL));
+    R("enddef", ncmpi_enddef(ncid));
+    R("enddef_again", ncmpi_enddef(ncid));
+    R("def_dim_in_data_mode", ncmpi_def_dim(ncid, "y", 4, &v));
+    R("put_global", ncmpi_put_vara_int_all(ncid, NC_GLOBAL, st, ct, i4));
+    R("put_bad_varid", ncmpi_put_vara_int_all(ncid, 77, st, ct, i4));
+    R("put_indep_in_coll_mode", ncmpi_put_vara_int(ncid, 0, st, ct, i4));
+    R("put_text_into_int", ncmpi_put_vara_text_all(ncid, 0, st, ct, "a"));
+    R("put_int_into_text", ncmpi_put_vara_int_all(ncid, vt, st, ct, i4));
+    R("put_start_out_of_bound", ncmpi_put_vara_int_all(ncid, 0, big, ct, i4));
+    R("put_start_negative", ncmpi_put_vara_int_all(ncid, 0, neg, ct, i4));
+    R("put_edge", ncmpi_put_vara_int_all(ncid, 0, st1, big, i4));
+    R("put_stride_zero", ncmpi_put_vars_int_all(ncid, 0, st, ct, sd0, i4));
+    R("get_rec_beyond_numrecs", ncmpi_get_vara_float_all(ncid, vr, st, ct, &f));
+    R("put_vara_null_count", ncmpi_put_vara_int_all(ncid, 0, st, NULL, i4));
+    R("flex_ignore_derived", ncmpi_put_vara_all(ncid, 0, st, ct, i4, NC_COUNT_IGNORE, MPI_2INT));
+    R("bput_no_buffer", ncmpi_bput_vara_int(ncid, 0, st, ct, i4, &req));
+    R("wait_indep_in_coll_mode", ncmpi_wait(ncid, NC_REQ_ALL, NULL, NULL));
+    R("begin_indep", ncmpi_begin_indep_data(ncid));
+    R("put_coll_in_indep_mode", ncmpi_put_vara_int_all(ncid, 0, st, ct, i4));
+    R("wait_all_in_indep_mode", ncmpi_wait_all(ncid, NC_REQ_ALL, NULL, NULL));
+    R("end_indep", ncmpi_end_indep_data(ncid));
+    R("redef", ncmpi_redef(ncid));
+    R("redef_again", ncmpi_redef(ncid));
+    R("del_att", ncmpi_del_att(ncid, NC_GLOBAL, "title"));
+    R("enddef2", ncmpi_enddef(ncid));
+    R("del_att_data_mode", ncmpi_del_att(ncid, NC_GLOBAL, "title"));
+    R("vard_deprecated", ncmpi_put_vard_all(ncid, 0, MPI_INT, i4, 1, MPI_INT));
+    R("malloc_size_disabled", ncmpi_inq_malloc_size(&st[0]));
+    R("close", ncmpi_close(ncid));
+    R("close_again", ncmpi_close(ncid));
+    R("open_missing", ncmpi_open(MPI_COMM_WORLD, "/nonexistent/x.nc", NC_NOWRITE, MPI_INFO_NULL, &ncid));
+    e = ncmpi_open(MPI_COMM_WORLD, path, NC_NOWRITE, MPI_INFO_NULL, &ncid);
+    R("open_ro", e);
+    R("put_read_only", ncmpi_put_vara_int_all(ncid, 0, st, ct, i4));
+    R("redef_read_only", ncmpi_redef(ncid));
+    {
+        int nd = -1, nv = -1, na = -1, ul = -2, fmt = -1;
+        MPI_Offset len = -1;
+        char name[NC_MAX_NAME + 1];
+        R("inq", ncmpi_inq(ncid, &nd, &nv, &na, &ul));
+        printf("inq_values %d %d %d %d\n", nd, nv, na, ul);
+        R("inq_format", ncmpi_inq_format(ncid, &fmt));
+        printf("format %d\n", fmt);
+        R("inq_dim", ncmpi_inq_dim(ncid, 1, name, &len));
+        printf("dim1 %s %lld\n", name, (long long)len);
+        R("inq_varname", ncmpi_inq_varname(ncid, 2, name));
+        printf("var2 %s\n", name);
+        R("inq_attlen", ncmpi_inq_attlen(ncid, NC_GLOBAL, "title", &len));
+        R("inq_num_rec_vars", ncmpi_inq_num_rec_vars(ncid, &nv));
+        printf("num_rec_vars %d\n", nv);
+    }
+    R("close_ro", ncmpi_close(ncid));
+#undef R
+    return 0;
+}
+
+static int mode_header(const char *path)
+{
+    int ncid, d[3], v[4];
+    CHECK(ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER | NC_64BIT_OFFSET, MPI_INFO_NULL, &ncid));
+    CHECK(ncmpi_put_att_text(ncid, NC_GLOBAL, "title", 14, "shared header"));
+    CHECK(ncmpi_def_dim(ncid, "time", NC_UNLIMITED, &d[0]));
+    CHECK(ncmpi_def_dim(ncid, "lat", 90, &d[1]));
+    CHECK(ncmpi_def_dim(ncid, "lon", 180, &d[2]));
+    CHECK(ncmpi_def_var(ncid, "temp", NC_FLOAT, 3, d, &v[0]));
+    CHECK(ncmpi_def_var(ncid, "lat", NC_DOUBLE, 1, &d[1], &v[1]));
+    CHECK(ncmpi_def_var(ncid, "flag", NC_BYTE, 2, &d[1], &v[2]));
+    CHECK(ncmpi_def_var(ncid, "name", NC_CHAR, 1, &d[2], &v[3]));
+    CHECK(ncmpi_put_att_text(ncid, v[0], "units", 1, "K"));
+    CHECK(ncmpi_enddef(ncid));
+    CHECK(ncmpi_redef(ncid));
+    CHECK(ncmpi_put_att_text(ncid, NC_GLOBAL, "history", 7, "redef'd"));
+    CHECK(ncmpi_enddef(ncid));
+    CHECK(ncmpi_close(ncid));
+    MPI_Allreduce(MPI_IN_PLACE, &nerrs, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);
+    return nerrs != 0;
+}
+
+int main(int argc, char **argv)
+{
+    int rc = 2;
+    MPI_Init(&argc, &argv);
+    if (argc >= 5 && strcmp(argv[1], "c1") == 0) rc = mode_c1(argv[2], argv[3], atoll(argv[4]));
+    else if (argc >= 7 && strcmp(argv[1], "putvara") == 0)
+        rc = mode_putvara(argv[2], atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), atoi(argv[6]),
+                          argc >= 8 ? atoi(argv[7]) : 0);
+    else if (argc >= 7 && strcmp(argv[1], "c4") == 0) rc = mode_c4(argv[2], argv[3], argv[4], atoll(argv[5]), atoi(argv[6]));
+    else if (argc >= 5 && strcmp(argv[1], "records") == 0) rc = mode_records(argv[2], atoll(argv[3]), atoll(argv[4]));
+    else if (argc >= 3 && strcmp(argv[1], "errors") == 0) rc = mode_errors(argv[2]);
+    else if (argc >= 3 && strcmp(argv[1], "header") == 0) rc = mode_header(argv[2]);
+    else fprintf(stderr, "usage: see the header of api_check.c\n");
+    MPI_Finalize();
+    return rc;
+}

@@ -51,7 +51,7 @@ def test_pncx_h_symbols_exported(built):
 def test_pncx_nc_h_symbols_exported(built):
     """file-level API (include/pncx_nc.h)"""
     decl = declared("pncx_nc.h")
-    assert len(decl) == 59
+    assert len(decl) == 63          # + create_shared, set_writer, set_numrecs, bput_varn (round 2)
     missing = [s for s in decl if s not in exported(LIB)]
     assert not missing, missing
 
