@@ -197,6 +197,52 @@ __device__ __forceinline__ void publish_status(int *status, bool bad, int value 
         __hip_atomic_store(status, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Where a kernel reports NC_ERANGE.  With every out-of-range wave storing
+// into one status word, the stores serialise at the memory side (about
+// 4.5 ns each): config 4's secondary variant -- 128 x 2^20 float -> NC_SHORT,
+// 18 % out of range, a fresh status value per call -- ran at 0.62 TB/s that
+// way, and at 6.08 TB/s (no status at all: 6.23) when each block writes the
+// call's epoch into a flag word of its own and a second kernel reduces the
+// flags (tools/publish_sweep.hip V0 vs V3, profiles/r02_publish_sweep.txt).
+// The launchers take a flag array per (device, stream) from sink_acquire
+// (pncx_kern_swap.hip); flags == nullptr falls back to the per-wave publish.
+struct Sink {
+    int *status;   // status word of a single launch (k_batch: per-segment words)
+    int *flags;    // per-block epoch flags of this launch, or nullptr
+    int  epoch;    // this launch's flag value (never reused on one stream)
+    int  sval;     // the value a status word gets
+};
+
+__device__ __forceinline__ void publish(const Sink &s, int *status, bool bad) {
+    if (s.flags != nullptr) {
+        // every thread of the block reaches this (kernels publish at the end)
+        if (__syncthreads_or(bad) && threadIdx.x == 0) s.flags[blockIdx.x] = s.epoch;
+    } else {
+        publish_status(status, bad, s.sval);
+    }
+}
+
+// the launcher side (pncx_kern_swap.hip)
+Sink sink_acquire(int *status, int sval, hipStream_t st, int64_t nblocks, bool want);
+int sink_finish(const Sink &s, hipStream_t st, int64_t nblocks, int err);
+int sink_finish_batch(const Sink &s, const pncxk_seg *dsegs, int nseg, int64_t nblocks, hipStream_t st, int err);
+
+// can a conversion from S to D report NC_ERANGE at all (get1/put1 rules):
+// into a floating type only double -> float is checked; from a floating type
+// into an integer always; integer -> integer when D's range does not hold S's
+template <class S, class D>
+constexpr bool range_loss() {
+    if constexpr (D::is_float) return S::is_float && S::size > D::size;
+    else if constexpr (S::is_float) return true;
+    else return S::lo < D::lo || S::hi > D::hi;
+}
+template <class Op> struct may_range { static constexpr bool value = true; };
+template <int ES> struct may_range<SwapOp<ES>> { static constexpr bool value = false; };
+template <int XT, int IT> struct may_range<GetOp<XT, IT>> { static constexpr bool value = range_loss<X<XT>, I<IT>>(); };
+template <int XT, int IT, bool P> struct may_range<PutOp<XT, IT, P>> {
+    static constexpr bool value = range_loss<I<IT>, X<XT>>();
+};
+
 // block -> segment of a batch grid: equal-size segments divide directly, a
 // few runs of equal sizes (e.g. NC_SHORT and NC_FLOAT variables) scan the
 // group table passed by value, anything else reads the device map
@@ -234,7 +280,7 @@ constexpr int64_t MAX_BLOCKS = 1LL << 23;
 template <class Op, bool NT>
 __global__ __launch_bounds__(256) void k_stream(const uint8_t *src, uint8_t *dst, int64_t head,
                                                 int64_t nvec, int64_t n,
-                                                typename Op::fill_t fill, int *status) {
+                                                typename Op::fill_t fill, Sink sk) {
     constexpr int SB = Op::VEC * Op::SS, DB = Op::VEC * Op::DS;
     const int64_t nb = gridDim.x;
     const int64_t tid = xcd_remap(blockIdx.x, nb) * 256 + threadIdx.x;
@@ -250,7 +296,7 @@ __global__ __launch_bounds__(256) void k_stream(const uint8_t *src, uint8_t *dst
     uint8_t *vd = dst + head * Op::DS;
     for (int64_t v = tid; v < nvec; v += stride) vec_step<Op, NT>(vs + v * SB, vd + v * DB, fill, bad);
 
-    publish_status(status, bad);
+    publish(sk, sk.status, bad);
 }
 
 // ---------------------------------------------------------------------------
@@ -373,7 +419,7 @@ __device__ __forceinline__ void scalar_range(const uint8_t *src, uint8_t *dst, i
 template <class Op, bool NT>
 __global__ __launch_bounds__(256) void k_tile(const uint8_t *src, uint8_t *dst, int64_t head,
                                               int64_t ntile, int64_t n, typename Op::fill_t fill,
-                                              int *status) {
+                                              Sink sk) {
     using S = Shape<Op>;
     __shared__ __attribute__((aligned(16))) uint8_t lds[S::USE_LDS ? 4096 : 16];
     bool bad = false;
@@ -389,18 +435,18 @@ __global__ __launch_bounds__(256) void k_tile(const uint8_t *src, uint8_t *dst, 
                           lds);
         if constexpr (S::USE_LDS) __syncthreads();       // LDS reuse in the next tile
     }
-    publish_status(status, bad);
+    publish(sk, sk.status, bad);
 }
 
 // fully scalar (misaligned buffers): one element per lane, byte-wise access
 template <class Op>
 __global__ __launch_bounds__(256) void k_scalar(const uint8_t *src, uint8_t *dst, int64_t n,
-                                                typename Op::fill_t fill, int *status) {
+                                                typename Op::fill_t fill, Sink sk) {
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     bool bad = false;
     for (int64_t e = tid; e < n; e += stride) scalar_elem<Op>(src, dst, e, fill, bad);
-    publish_status(status, bad);
+    publish(sk, sk.status, bad);
 }
 
 // ---------------------------------------------------------------------------
@@ -416,7 +462,7 @@ constexpr int BATCH_STEPS = 1;  // tiles per block
 
 template <class Op, bool NT>
 __global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg, long long uniform,
-                                               const int *map, pncxk_groups grp, int sval) {
+                                               const int *map, pncxk_groups grp, Sink sk) {
     using S = Shape<Op>;
     __shared__ __attribute__((aligned(16))) uint8_t lds[S::USE_LDS ? 4096 : 16];
     const long long b = blockIdx.x;
@@ -435,7 +481,7 @@ __global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg, 
     if (rel < ntile)
         tile_body<Op, NT>(src + (sg.head + rel * (int64_t)S::TILE) * S::SS,
                           dst + (sg.head + rel * (int64_t)S::TILE) * S::DS, fill, bad, lds);
-    publish_status(sg.status, bad, sval);
+    publish(sk, sg.status, bad);
 }
 
 // ---------------------------------------------------------------------------
@@ -496,7 +542,7 @@ constexpr int IMAP_U = 4;
 // GATHER = true: src strided (user, put); false: dst strided (user, get)
 template <class Op, bool GATHER, typename IDX>
 __global__ __launch_bounds__(256) void k_imap(const uint8_t *src, uint8_t *dst, int64_t n, pncxk_imap m,
-                                              typename Op::fill_t fill, int *status) {
+                                              typename Op::fill_t fill, Sink sk) {
     using SU = typename Op::SU;
     using DU = typename Op::DU;
     constexpr int UES = GATHER ? Op::SS : Op::DS;      // user element size
@@ -535,7 +581,7 @@ __global__ __launch_bounds__(256) void k_imap(const uint8_t *src, uint8_t *dst, 
             }
         }
     }
-    publish_status(status, bad);
+    publish(sk, sk.status, bad);
 }
 
 // Derived buftype in packed order with long runs (tmode 3, or uniform runs
@@ -544,7 +590,7 @@ __global__ __launch_bounds__(256) void k_imap(const uint8_t *src, uint8_t *dst, 
 // along the piece -- both sides contiguous, no search.  c = copy, b = piece.
 template <class Op, bool GATHER>
 __global__ __launch_bounds__(256) void k_tmap_runs(const uint8_t *src, uint8_t *dst, int64_t n, pncxk_imap m,
-                                                   typename Op::fill_t fill, int *status) {
+                                                   typename Op::fill_t fill, Sink sk) {
     using SU = typename Op::SU;
     using DU = typename Op::DU;
     constexpr int UES = GATHER ? Op::SS : Op::DS;
@@ -579,7 +625,7 @@ __global__ __launch_bounds__(256) void k_tmap_runs(const uint8_t *src, uint8_t *
             }
         }
     }
-    publish_status(status, bad);
+    publish(sk, sk.status, bad);
 }
 
 // ---------------------------------------------------------------------------
@@ -673,7 +719,7 @@ __device__ __forceinline__ void xpose_tile(const uint8_t *src, uint8_t *dst, con
 // Otherwise the bounds-checked loops below with unaligned accesses.
 template <class Op, bool GATHER, bool ALIGNED>
 __global__ __launch_bounds__(256) void k_imap_tile(const uint8_t *src, uint8_t *dst, TransposeGeom g,
-                                                   typename Op::fill_t fill, int *status) {
+                                                   typename Op::fill_t fill, Sink sk) {
     using SU = typename Op::SU;
     using DU = typename Op::DU;
     using TU = typename std::conditional<GATHER, SU, DU>::type;     // LDS holds user-side bits
@@ -744,7 +790,7 @@ __global__ __launch_bounds__(256) void k_imap_tile(const uint8_t *src, uint8_t *
         }
         __syncthreads();
     }
-    publish_status(status, bad);
+    publish(sk, sk.status, bad);
 }
 
 // Pick the transpose kernel for a varm layout: P = last dim, U = the other
@@ -790,6 +836,7 @@ int launch_imap(const pncxk_args *a, const pncxk_imap *m, int gather) {
     const typename Op::fill_t fill = (typename Op::fill_t)a->fill;
     hipStream_t st = (hipStream_t)a->stream;
     TransposeGeom g;
+    const bool want = may_range<Op>::value && a->status != nullptr;
     // run-major: long-run tables in packed order, and uniform runs of 256..4096
     // elements in packed order (one wave per run instead of a division per
     // element; with 64-element runs the per-wave setup made it slower:
@@ -797,34 +844,37 @@ int launch_imap(const pncxk_args *a, const pncxk_imap *m, int gather) {
     if (m->tmode == 3 || (m->tmode == 1 && m->ndims == 1 && m->imap[0] == 1 && m->tlen >= 256 && m->tlen <= 4096)) {
         const int64_t pieces = a->n / m->tn * m->tnblk;
         const unsigned grid = (unsigned)((pieces + 3) / 4 < MAX_BLOCKS ? (pieces + 3) / 4 : MAX_BLOCKS);
-        if (gather) hipLaunchKernelGGL((k_tmap_runs<Op, true>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, a->status);
-        else hipLaunchKernelGGL((k_tmap_runs<Op, false>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, a->status);
-        return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
+        const Sink sk = sink_acquire(a->status, NC_ERANGE, st, grid, want);
+        if (gather) hipLaunchKernelGGL((k_tmap_runs<Op, true>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, sk);
+        else hipLaunchKernelGGL((k_tmap_runs<Op, false>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, sk);
+        return sink_finish(sk, st, grid, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
     }
     if (transpose_geom(m, &g)) {
         const unsigned grid = (unsigned)(g.ntiles < MAX_BLOCKS ? g.ntiles : MAX_BLOCKS);
         const int ues = gather ? Op::SS : Op::DS, pes = gather ? Op::DS : Op::SS;
         const bool al = (uintptr_t)src % (uintptr_t)(gather ? ues : pes) == 0 &&
                         (uintptr_t)dst % (uintptr_t)(gather ? pes : ues) == 0;
+        const Sink sk = sink_acquire(a->status, NC_ERANGE, st, grid, want);
         if (gather) {
-            if (al) hipLaunchKernelGGL((k_imap_tile<Op, true, true>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, a->status);
-            else hipLaunchKernelGGL((k_imap_tile<Op, true, false>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, a->status);
+            if (al) hipLaunchKernelGGL((k_imap_tile<Op, true, true>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, sk);
+            else hipLaunchKernelGGL((k_imap_tile<Op, true, false>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, sk);
         } else {
-            if (al) hipLaunchKernelGGL((k_imap_tile<Op, false, true>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, a->status);
-            else hipLaunchKernelGGL((k_imap_tile<Op, false, false>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, a->status);
+            if (al) hipLaunchKernelGGL((k_imap_tile<Op, false, true>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, sk);
+            else hipLaunchKernelGGL((k_imap_tile<Op, false, false>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, sk);
         }
-        return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
+        return sink_finish(sk, st, grid, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
     }
     const int grid = launch_grid(a->n, 4);
     const bool small = a->n < (1LL << 32) && m->max_count < (1LL << 32);
+    const Sink sk = sink_acquire(a->status, NC_ERANGE, st, grid, want);
     if (gather) {
-        if (small) hipLaunchKernelGGL((k_imap<Op, true, uint32_t>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, a->status);
-        else hipLaunchKernelGGL((k_imap<Op, true, uint64_t>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, a->status);
+        if (small) hipLaunchKernelGGL((k_imap<Op, true, uint32_t>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, sk);
+        else hipLaunchKernelGGL((k_imap<Op, true, uint64_t>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, sk);
     } else {
-        if (small) hipLaunchKernelGGL((k_imap<Op, false, uint32_t>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, a->status);
-        else hipLaunchKernelGGL((k_imap<Op, false, uint64_t>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, a->status);
+        if (small) hipLaunchKernelGGL((k_imap<Op, false, uint32_t>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, sk);
+        else hipLaunchKernelGGL((k_imap<Op, false, uint64_t>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, sk);
     }
-    return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
+    return sink_finish(sk, st, grid, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
 }
 
 // ---------------------------------------------------------------------------
@@ -852,38 +902,46 @@ int launch_stream(const pncxk_args *a) {
     const uint8_t *src = (const uint8_t *)a->src;
     uint8_t *dst = (uint8_t *)a->dst;
     const typename Op::fill_t fill = (typename Op::fill_t)a->fill;
+    const bool want = may_range<Op>::value && a->status != nullptr;
+    int64_t grid;
+    Sink sk;
     if (h < 0) {
-        const int grid = launch_grid(n, 1);
-        hipLaunchKernelGGL((k_scalar<Op>), dim3(grid), dim3(256), 0, st, src, dst, n, fill, a->status);
+        grid = launch_grid(n, 1);
+        sk = sink_acquire(a->status, NC_ERANGE, st, grid, want);
+        hipLaunchKernelGGL((k_scalar<Op>), dim3((unsigned)grid), dim3(256), 0, st, src, dst, n, fill, sk);
     } else if constexpr (Op::PRESERVE) {
         // NULL-fill codecs read xbuf: interleaved layout, plain stores
         const int64_t nvec = (n - h) / Op::VEC;
-        int64_t grid = (nvec + 255) / 256;
+        grid = (nvec + 255) / 256;
         if (grid < 1) grid = 1;
         if (grid > MAX_BLOCKS) grid = MAX_BLOCKS;
+        sk = sink_acquire(a->status, NC_ERANGE, st, grid, want);
         hipLaunchKernelGGL((k_stream<Op, false>), dim3((unsigned)grid), dim3(256), 0, st, src, dst, h,
-                           nvec, n, fill, a->status);
+                           nvec, n, fill, sk);
     } else {
         const int64_t ntile = (n - h) / Shape<Op>::TILE;
-        int64_t grid = ntile < 1 ? 1 : ntile;
+        grid = ntile < 1 ? 1 : ntile;
         if (grid > MAX_BLOCKS) grid = MAX_BLOCKS;
+        sk = sink_acquire(a->status, NC_ERANGE, st, grid, want);
         if (a->nontemporal >= 0)
             hipLaunchKernelGGL((k_tile<Op, true>), dim3((unsigned)grid), dim3(256), 0, st, src, dst, h,
-                               ntile, n, fill, a->status);
+                               ntile, n, fill, sk);
         else
             hipLaunchKernelGGL((k_tile<Op, false>), dim3((unsigned)grid), dim3(256), 0, st, src, dst, h,
-                               ntile, n, fill, a->status);
+                               ntile, n, fill, sk);
     }
-    return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
+    return sink_finish(sk, st, grid, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
 }
 
 template <class Op>
 int launch_batch(const pncxk_batch_args *a) {
     if (a->nblocks <= 0) return 0;
     if constexpr (Op::PRESERVE) return NC_EINVAL;   // host runs these one by one
-    hipLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0,
-                       (hipStream_t)a->stream, a->dsegs, a->nseg, a->uniform, a->dmap, a->grp, a->sval);
-    return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
+    hipStream_t st = (hipStream_t)a->stream;
+    const Sink sk = sink_acquire(nullptr, a->sval, st, a->nblocks, may_range<Op>::value);
+    hipLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0, st, a->dsegs, a->nseg,
+                       a->uniform, a->dmap, a->grp, sk);
+    return sink_finish_batch(sk, a->dsegs, a->nseg, a->nblocks, st, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
 }
 
 template <class Op>

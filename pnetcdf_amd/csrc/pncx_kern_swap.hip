@@ -4,6 +4,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+
 #include "pncx_kern.hpp"
 
 using namespace pncx;
@@ -128,6 +130,158 @@ extern "C" int pncxk_fill(void *dst, long long nelems, int xsize, const void *xv
                        head, nvec, pattern, xv, xsize);
     return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
 }
+
+// ---------------------------------------------------------------------------
+// NC_ERANGE reporting through per-block flags (see Sink in pncx_kern.hpp).
+// A flag array belongs to one (device, stream): calls on one stream run in
+// order, so each call's epoch is new to its array and no zeroing is needed;
+// calls on different streams never share an array (sharing one would let a
+// later call overwrite an earlier call's flags before its reduce reads them).
+// The mutex is held from sink_acquire to sink_finish so that one call's
+// kernel and reduce are enqueued back to back.
+// ---------------------------------------------------------------------------
+namespace {
+struct FlagSlot {
+    int dev;
+    hipStream_t stream;
+    int *flags;
+    int64_t cap;          // ints
+    int epoch;
+    hipEvent_t done;      // recorded after the last reduce that read this array
+    uint64_t tick;
+    bool live;
+};
+constexpr int NFLAGSLOT = 32;
+FlagSlot g_fslot[NFLAGSLOT];
+std::mutex g_fslot_mu;
+uint64_t g_ftick;
+}  // namespace
+
+namespace pncx {
+
+Sink sink_acquire(int *status, int sval, hipStream_t st, int64_t nblocks, bool want) {
+    Sink s{status, nullptr, 0, sval};
+    if (!want || nblocks <= 0) return s;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return s;
+    g_fslot_mu.lock();
+    FlagSlot *f = nullptr, *lru = nullptr;
+    for (int i = 0; i < NFLAGSLOT; i++) {
+        FlagSlot *c = &g_fslot[i];
+        if (c->live && c->dev == dev && c->stream == st) { f = c; break; }
+        if (lru == nullptr || !c->live || (lru->live && c->tick < lru->tick)) lru = c;
+    }
+    if (f == nullptr) {                 // take a free slot, or the least recently used one
+        f = lru;
+        if (f->live) {
+            (void)hipEventSynchronize(f->done);       // its last reduce has read the flags
+            if (f->dev != dev) {
+                (void)hipFree(f->flags);
+                (void)hipEventDestroy(f->done);
+                f->flags = nullptr;
+                f->cap = 0;
+                f->done = nullptr;
+            }
+        }
+        f->live = true;
+        f->dev = dev;
+        f->stream = st;     /* the epoch counter continues: the array may hold old epochs */
+        if (f->done == nullptr && hipEventCreateWithFlags(&f->done, hipEventDisableTiming) != hipSuccess) {
+            f->done = nullptr;
+            f->live = false;
+            g_fslot_mu.unlock();
+            return s;
+        }
+    }
+    if (f->cap < nblocks) {             // grow: wait for the array's last use on this stream
+        (void)hipEventSynchronize(f->done);
+        if (f->flags) (void)hipFree(f->flags);
+        f->cap = nblocks > 2 * f->cap ? nblocks : 2 * f->cap;
+        if (hipMalloc(&f->flags, sizeof(int) * (size_t)f->cap) != hipSuccess ||
+            hipMemsetAsync(f->flags, 0, sizeof(int) * (size_t)f->cap, st) != hipSuccess) {
+            (void)hipGetLastError();
+            f->flags = nullptr;
+            f->cap = 0;
+            g_fslot_mu.unlock();
+            return s;                   // per-wave publish
+        }
+    }
+    if (++f->epoch >= 0x3fffffff) {     // epochs must not repeat on this array
+        if (hipMemsetAsync(f->flags, 0, sizeof(int) * (size_t)f->cap, st) != hipSuccess) {
+            g_fslot_mu.unlock();
+            return s;
+        }
+        f->epoch = 1;
+    }
+    f->tick = ++g_ftick;
+    s.flags = f->flags;
+    s.epoch = f->epoch;
+    return s;                           // the mutex stays held until sink_finish*
+}
+
+static void sink_release(hipStream_t st) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    for (int i = 0; i < NFLAGSLOT; i++)
+        if (g_fslot[i].live && g_fslot[i].dev == dev && g_fslot[i].stream == st) {
+            (void)hipEventRecord(g_fslot[i].done, st);
+            break;
+        }
+    g_fslot_mu.unlock();
+}
+
+}  // namespace pncx
+
+// single status word: any flag of this launch's epoch -> *status = sval
+__global__ __launch_bounds__(256) void k_flags_one(const int *flags, int64_t nb, int epoch, int *status, int sval) {
+    bool hit = false;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += (int64_t)gridDim.x * 256)
+        hit |= flags[i] == epoch;
+    if (__syncthreads_or(hit) && threadIdx.x == 0 &&
+        __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != sval)
+        __hip_atomic_store(status, sval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// batch: one block per segment over its blocks [block0, next block0)
+__global__ __launch_bounds__(256) void k_flags_batch(const pncxk_seg *segs, int nseg, int64_t nb, const int *flags,
+                                                     int epoch, int sval) {
+    const int s = blockIdx.x;
+    if (s >= nseg) return;                 // whole block leaves together
+    const int64_t b0 = segs[s].block0, b1 = s + 1 < nseg ? segs[s + 1].block0 : nb;
+    bool hit = false;
+    for (int64_t b = b0 + threadIdx.x; b < b1; b += 256) hit |= flags[b] == epoch;
+    int *st = segs[s].status;
+    if (__syncthreads_or(hit) && threadIdx.x == 0 && st != nullptr) *st = sval;
+}
+
+namespace pncx {
+
+int sink_finish(const Sink &s, hipStream_t st, int64_t nblocks, int err) {
+    if (s.flags == nullptr) return err;
+    if (!err) {
+        int64_t g = (nblocks + 255) / 256;       /* one flag per lane up to 2^18 blocks */
+        if (g > 1024) g = 1024;
+        if (g < 1) g = 1;
+        hipLaunchKernelGGL(k_flags_one, dim3((unsigned)g), dim3(256), 0, st, s.flags, nblocks, s.epoch, s.status,
+                           s.sval);
+        if (hipGetLastError() != hipSuccess) err = PNCX_EDEVICE;
+    }
+    sink_release(st);
+    return err;
+}
+
+int sink_finish_batch(const Sink &s, const pncxk_seg *dsegs, int nseg, int64_t nblocks, hipStream_t st, int err) {
+    if (s.flags == nullptr) return err;
+    if (!err && nseg > 0) {
+        hipLaunchKernelGGL(k_flags_batch, dim3((unsigned)nseg), dim3(256), 0, st, dsegs, nseg, nblocks, s.flags,
+                           s.epoch, s.sval);
+        if (hipGetLastError() != hipSuccess) err = PNCX_EDEVICE;
+    }
+    sink_release(st);
+    return err;
+}
+
+}  // namespace pncx
 
 // batch / opinfo dispatch: get and put live in their own TUs
 extern "C" int pncxk_batch_get(int xtype, int itype, const pncxk_batch_args *a);

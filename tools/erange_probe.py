@@ -29,6 +29,8 @@ def main():
     dstat = torch.zeros(nseg, dtype=torch.int32, device="cuda")
     out = []
     for name in ("bits", "u40000", "u30000", "u40000_sorted"):
+        st.zero_()
+        dstat.zero_()
         if name == "bits":
             src.view(torch.int32).random_()
         elif name.startswith("u40000"):
@@ -37,9 +39,13 @@ def main():
                 src.copy_(src.sort().values)
         else:
             src.uniform_(-30000, 30000)
-        for kind in ("tile", "batch", "batch_async"):
+        for kind in ("tile", "tile_fresh", "batch", "batch_async", "batch_async_fresh"):
             def run():
-                if kind == "tile":
+                if kind == "tile_fresh":
+                    st.zero_()
+                if kind == "batch_async_fresh":
+                    dstat.zero_()
+                if kind.startswith("tile"):
                     rc = lib.pncx_dev_putn(5, T.NC_SHORT, ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()),
                                            n, T.ITYPE_FLOAT, fp, ctypes.c_void_p(st.data_ptr()), sp)
                 elif kind == "batch":
@@ -47,6 +53,7 @@ def main():
                 else:
                     rc = lib.pncx_dev_batch_async(segs, nseg, ctypes.c_void_p(dstat.data_ptr()), sp)
                 assert rc in (0, T.NC_ERANGE), rc
+            # statuses must still be right: every segment of u40000 / bits has ERANGE
             for _ in range(3):
                 run()
             torch.cuda.synchronize()
@@ -57,7 +64,15 @@ def main():
                 b.record()
             torch.cuda.synchronize()
             ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
-            out.append({"input": name, "kernel": kind, "ms": round(ms, 4), "GBps": round(6 * n / ms / 1e6, 1)})
+            want = name != "u30000"
+            if kind.startswith("tile"):
+                ok = (int(st.item()) == T.NC_ERANGE) == want
+            elif kind == "batch":
+                ok = all((v == T.NC_ERANGE) == want for v in stv)
+            else:
+                ok = all((v == T.NC_ERANGE) == want for v in dstat.cpu().tolist())
+            out.append({"input": name, "kernel": kind, "ms": round(ms, 4), "GBps": round(6 * n / ms / 1e6, 1),
+                        "status_ok": ok})
             print(json.dumps(out[-1]), flush=True)
 
 
