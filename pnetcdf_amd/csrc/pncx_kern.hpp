@@ -34,12 +34,18 @@ __device__ __forceinline__ u32x4 ld16(const uint8_t *p) {
 // r01_swap_sweep_store_policy.txt).  No builtin exposes sc1 on a global
 // store, hence the vector-store inline asm; nothing in these kernels reads
 // what it stores, so the compiler's wait counting needs no view of it.
+// What the compiler cannot see is the store-data hazard: on gfx940+ a VALU
+// write to the VGPRs of a store with more than 64 bits of data needs 2 wait
+// states (LLVM inserts them for its own stores, GCNHazardRecognizer), and a
+// register reused right after this asm store corrupted the first 8 bytes of
+// 16 (k_tile<PutOp<NC_FLOAT, double>>, round 2).  The s_nop 1 inside the asm
+// provides them; 64-bit stores have no such hazard.
 template <typename T>
 __device__ __forceinline__ void st_stream(uint8_t *p, T v) {
     if constexpr (sizeof(T) == 16) {
         u32x4 w;
         __builtin_memcpy(&w, &v, 16);
-        asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(p), "v"(w) : "memory");
+        asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
     } else if constexpr (sizeof(T) == 8) {
         uint64_t w;
         __builtin_memcpy(&w, &v, 8);

@@ -656,3 +656,40 @@ def test_c3_full_size_int_to_double(torch_cuda):
     for s in range(0, n, step):
         native = xr[s:s + step].view(torch.uint8).view(-1, 4).flip(1).reshape(-1).view(torch.int32)
         assert torch.equal(dst[s:s + step], native.to(torch.float64))
+
+
+@pytest.mark.slow
+def test_large_conversions_every_element(torch_cuda):
+    """k_tile over 2^25 elements (32768 blocks; the one-shot grid) for a
+    narrowing, a widening and a same-size conversion, every element against
+    torch on the device.  Guards the store-data hazard of the inline-asm
+    streaming store (round 2: a VALU reuse of the data VGPRs two
+    instructions after global_store_dwordx4 corrupted 8 of 16 bytes in
+    k_tile<PutOp<NC_FLOAT, double>> at random places)."""
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    n = 1 << 25
+    g = torch.Generator(device="cuda").manual_seed(5)
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+    def be(t):                       # native tensor -> its big-endian bytes
+        es = t.element_size()
+        return t.contiguous().view(torch.uint8).view(-1, es).flip(1).reshape(-1)
+
+    for rep in range(3):
+        d = torch.randn(n, dtype=torch.float64, device="cuda", generator=g) * 1e3
+        x = torch.empty(n * 4, dtype=torch.uint8, device="cuda")          # double -> NC_FLOAT (narrowing)
+        pncx.dev_putn(5, T.NC_FLOAT, x, d, n, T.ITYPE_DOUBLE, T.fill_bytes(T.NC_FLOAT), st)
+        torch.cuda.synchronize()
+        assert int(st.item()) == 0 and torch.equal(x, be(d.float())), rep
+        i32 = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device="cuda", generator=g)
+        xi = be(i32)
+        o = torch.empty(n, dtype=torch.float64, device="cuda")            # NC_INT -> double (widening)
+        pncx.dev_getn(5, T.NC_INT, xi, o, n, T.ITYPE_DOUBLE, st)
+        torch.cuda.synchronize()
+        assert torch.equal(o, i32.double()), rep
+        f = torch.randn(n, dtype=torch.float32, device="cuda", generator=g)
+        of = torch.empty(n, dtype=torch.float32, device="cuda")           # NC_FLOAT -> float (swap)
+        pncx.dev_getn(5, T.NC_FLOAT, be(f), of, n, T.ITYPE_FLOAT, st)
+        torch.cuda.synchronize()
+        assert torch.equal(of, f), rep

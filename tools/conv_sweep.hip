@@ -21,7 +21,7 @@ template <class T, bool NT> __device__ __forceinline__ T ld(const T *p) {
 template <class T, bool NT> __device__ __forceinline__ void st(T *p, T v) {
 #ifdef SC1
     if constexpr (NT && sizeof(T) == 16) {
-        asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(p), "v"(v) : "memory");
+        asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
         return;
     } else if constexpr (NT && sizeof(T) == 8) {
         asm volatile("global_store_dwordx2 %0, %1, off nt sc1" ::"v"(p), "v"(v) : "memory");

@@ -123,9 +123,9 @@ template <int SP>
 __device__ __forceinline__ void st_pol(u32x4 *p, u32x4 v) {
     if constexpr (SP == 0) __builtin_nontemporal_store(v, p);
     else if constexpr (SP == 1) *p = v;
-    else if constexpr (SP == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
-    else if constexpr (SP == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(p), "v"(v) : "memory");
-    else asm volatile("global_store_dwordx4 %0, %1, off nt sc1" :: "v"(p), "v"(v) : "memory");
+    else if constexpr (SP == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
+    else if constexpr (SP == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
 }
 template <int U, int BS, int SP, bool RM = true>
 __global__ __launch_bounds__(BS) void k_one3(u32x4 *p, int64_t nvec) {
