@@ -322,7 +322,7 @@ class C4Batch(Workload):
         self.slab_per_elem = 3
         self.metric_key = "batch_c4_erange" if self._erange else "batch_c4"
         self.dtype = "f32->i16/f32" if self._erange else "i16/f32"
-        self.kernel = ("k_batch<PutOp<NC_SHORT, float>> + k_batch<SwapOp<4>>" if self._erange
+        self.kernel = ("k_batch<PutOp<NC_SHORT, float>> + k_batch_swapmix" if self._erange
                        else "k_batch_swapmix")
         self.cfg = {"workload": ("C4 secondary: iput_vara batch, 128 NC_SHORT vars from float in [-40000, 40000] "
                                  "(~18% NC_ERANGE + fill) + 128 NC_FLOAT vars, 2^20 elements each" if self._erange
