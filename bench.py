@@ -360,32 +360,43 @@ def make_workload(name, torch, lib, sptr, args, world, rank):
 def measure(torch, lib, group, stream, wl, steps, warmup):
     """W untimed warmups, then K steps between barrier + synchronize; HIP
     events on the kernel's stream around every launch (for the synchronous
-    batch call the library's own events around its kernels).  Returns
+    batch call the library's own kernel events, in a second pass).  Returns
     (max-over-ranks wall seconds, kernel ms per launch, call ms or None)."""
     torch.cuda.synchronize()
     for _ in range(warmup):
         wl.launch()
     torch.cuda.synchronize()
-    if wl.lib_timed:
-        lib.pncx_dev_batch_timing(1)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    # The synchronous batch call returns after its kernels, so the wall clock
+    # times the calls; the library's kernel events (stamped by the kernels'
+    # own dispatches) add ~9 us to each synchronous call, so they run in a
+    # second pass of the same K calls (tools/c4_call_probe.py, DESIGN.md).
+    evs = [] if wl.lib_timed else \
+        [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     group.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(steps):
-        evs[k][0].record(stream)
-        wl.launch()
-        evs[k][1].record(stream)
+    if wl.lib_timed:
+        for k in range(steps):
+            wl.launch()
+    else:
+        for k in range(steps):
+            evs[k][0].record(stream)
+            wl.launch()
+            evs[k][1].record(stream)
     torch.cuda.synchronize()
     group.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / steps
     call_ms = None
     if wl.lib_timed:
+        lib.pncx_dev_batch_timing(1)
+        for k in range(steps):
+            wl.launch()
         tot, calls = ctypes.c_double(), ctypes.c_longlong()
         assert lib.pncx_dev_batch_kernel_ms(ctypes.byref(tot), ctypes.byref(calls)) == 0 and calls.value == steps
-        call_ms, kern_ms = kern_ms, tot.value / calls.value
+        call_ms, kern_ms = elapsed * 1e3 / steps, tot.value / calls.value
         lib.pncx_dev_batch_timing(0)
+    else:
+        kern_ms = sum(a.elapsed_time(b) for a, b in evs) / steps
     elapsed, kern_ms = group.max([elapsed, kern_ms])
     return elapsed, kern_ms, call_ms
 

@@ -267,6 +267,7 @@ int pncx_dev_status_read(const int *dstatus, pncx_stream_t stream)
 #define NSLOT 2
 #define MAX_DEV 64
 
+#define NTEV 256              /* event pairs of pncx_dev_batch_timing read in one go */
 typedef struct ctx_t {
     int    init;
     void  *stream[NSLOT];
@@ -297,9 +298,13 @@ typedef struct ctx_t {
                                * segment array only its address */
     struct cls_t *cache_cls;
     size_t cache_soff, cache_moff;
-    void  *ev;                /* completion event for the spin-wait */
+    int   *hdone_h, *hdone_d; /* host-mapped completion word [0] + statuses [16..]
+                               * of the synchronous pncx_dev_batch (host / device address) */
+    int    hdone_cap;         /* status words it holds */
+    int    done_seq;
     int    timing;            /* pncx_dev_batch_timing: events around the batch kernels */
-    void  *tev0, *tev1;
+    void  *tev[2 * NTEV];     /* start/stop event pairs of the timed calls not yet read */
+    int    tpend;             /* pairs in use */
     double tms;               /* summed kernel time of the timed batch calls */
     long long tcalls;         /* ... and their number                         */
     unsigned long long *dfirst;   /* pncx_dev_first_diff result word */
@@ -1310,14 +1315,27 @@ static int batch_plan(plan_t *p)
 /* scratch layout (device and pinned mirror): [statuses | descriptors | maps].
  * ONE upload zeroes the statuses and installs the descriptors; then the
  * unbatched items and the class kernels run; one copy brings the statuses back. */
-/* pncx_dev_batch_timing: add the kernel time of the call that just completed */
+/* pncx_dev_batch_timing: the event pairs are read when NTEV are in use or
+ * when pncx_dev_batch_kernel_ms asks (reading them per call would add a
+ * synchronize and an elapsed-time query to every timed call) */
+static void batch_time_drain(ctx_t *c)
+{
+    int k;
+    for (k = 0; k < c->tpend; k++) {
+        float ms = 0.0f;
+        if (pncxrt_event_sync(c->tev[2 * k + 1]) == 0 &&
+            pncxrt_event_elapsed_ms(&ms, c->tev[2 * k], c->tev[2 * k + 1]) == 0) {
+            c->tms += ms;
+            c->tcalls++;
+        }
+    }
+    c->tpend = 0;
+}
+
+/* the call that used pair tpend has completed */
 static void batch_time(ctx_t *c)
 {
-    float ms = 0.0f;
-    if (pncxrt_event_elapsed_ms(&ms, c->tev0, c->tev1) == 0) {
-        c->tms += ms;
-        c->tcalls++;
-    }
+    if (++c->tpend == NTEV) batch_time_drain(c);
 }
 
 /* launch the class kernels of a plan whose descriptors are on the device */
@@ -1325,7 +1343,12 @@ static int launch_classes(const cls_t *cls, int ncls, uint8_t *dbase, size_t sof
                           int build_maps, void *stream, ctx_t *tc)
 {
     int k, err = 0;
-    if (tc != NULL && tc->timing) err = pncxrt_event_record(tc->tev0, stream);
+    /* timing: the start event is stamped by the first class kernel's own
+     * dispatch (hipExtLaunchKernel), not recorded ahead of it -- on an idle
+     * stream a recorded event would also time the host's launch call */
+    const int timed = tc != NULL && tc->timing;
+    void *ev0 = timed ? tc->tev[2 * tc->tpend] : NULL, *ev1 = timed ? tc->tev[2 * tc->tpend + 1] : NULL;
+    if (timed && ncls == 0) err = pncxrt_event_record(ev0, stream);
     pncxk_seg *dseg = (pncxk_seg *)(dbase + soff);
     int *dmap = (int *)(dbase + moff);
     for (k = 0; k < ncls && !err; k++) {
@@ -1339,10 +1362,13 @@ static int launch_classes(const cls_t *cls, int ncls, uint8_t *dbase, size_t sof
         ba.grp = c->grp;
         ba.sval = sval;
         ba.stream = stream;
+        ba.ev_start = ba.ev_stop = NULL;
         if (ba.dmap != NULL && build_maps) err = pncxk_batch_map(&ba);
+        if (timed && k == 0) ba.ev_start = ev0;
+        if (timed && k == ncls - 1) ba.ev_stop = ev1;
         if (!err) err = pncxk_batch(c->op.kind, c->op.a, c->op.b, c->op.c, &ba);
     }
-    if (!err && tc != NULL && tc->timing) err = pncxrt_event_record(tc->tev1, stream);
+    if (!err && timed && ncls == 0) err = pncxrt_event_record(ev1, stream);
     return err;
 }
 
@@ -1370,26 +1396,37 @@ static int batch_run(plan_t *p, int nseg, uint8_t *dbase, uint8_t *hbase, size_t
     return err;
 }
 
-/* Wait for the work queued on `stream`: spin on an event for up to 20 ms
- * (a blocking wait adds a wake-up of ~10 us to every batch call), then block. */
-static int spin_wait(ctx_t *c, void *stream)
+/* Completion of a synchronous batch: one block copies the n status words
+ * into host-mapped memory and then sets the completion word, which the host
+ * polls for up to 20 ms before it blocks on the stream.  Returns with the
+ * statuses at c->hdone_h + 16. */
+static int done_wait(ctx_t *c, const int *dstat, int n, void *stream)
 {
     struct timespec t0, t;
-    int r;
-    if (c->ev == NULL && pncxrt_event_create(&c->ev) != 0) {
-        c->ev = NULL;
-        return pncxrt_stream_sync(stream);
+    int seq, err;
+    if (c->hdone_cap < n || c->hdone_h == NULL) {
+        void *h, *d;
+        const int cap = n < 1024 ? 1024 : 2 * n;
+        pncxrt_host_free(c->hdone_h);         /* no completion kernel is outstanding */
+        c->hdone_h = c->hdone_d = NULL;
+        c->hdone_cap = 0;
+        if (pncxrt_host_alloc_mapped(&h, &d, sizeof(int) * (size_t)(16 + cap)) != 0) return PNCX_EDEVICE;
+        c->hdone_h = (int *)h;
+        c->hdone_d = (int *)d;
+        c->hdone_cap = cap;
+        __atomic_store_n(c->hdone_h, 0, __ATOMIC_RELEASE);
     }
-    if (pncxrt_event_record(c->ev, stream) != 0) return PNCX_EDEVICE;
+    seq = c->done_seq = (c->done_seq + 1) & 0x7fffffff;
+    if (seq == 0) seq = c->done_seq = 1;
+    if ((err = pncxk_batch_done(dstat, n, c->hdone_d + 16, c->hdone_d, seq, stream)) != 0) return err;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (;;) {
-        r = pncxrt_event_query(c->ev);
-        if (r == 1) return 0;
-        if (r < 0) return r;
+        if (__atomic_load_n(c->hdone_h, __ATOMIC_ACQUIRE) == seq) return 0;
         clock_gettime(CLOCK_MONOTONIC, &t);
         if ((t.tv_sec - t0.tv_sec) * 1000000000LL + (t.tv_nsec - t0.tv_nsec) > 20000000LL) break;
     }
-    return pncxrt_event_sync(c->ev);
+    if ((err = pncxrt_stream_sync(stream)) != 0) return err;
+    return __atomic_load_n(c->hdone_h, __ATOMIC_ACQUIRE) == seq ? 0 : PNCX_EDEVICE;
 }
 
 /* the fill value a put segment's plan was classified with (classify copies
@@ -1446,14 +1483,12 @@ static int dev_batch(const pncx_seg *segs, int nseg, int *status_out, int *dstat
             c->async_stream = stream;
         }
         if (!async) {
-            /* byte swaps and copies never raise NC_ERANGE: no status read-back */
-            if (!err && !c->cache_swaponly)
-                err = pncxrt_memcpy_d2h(c->hscratch, c->dscratch, sizeof(int) * (size_t)nseg, stream);
-            if (!err) err = spin_wait(c, stream);
+            /* byte swaps and copies never raise NC_ERANGE: no statuses to bring back */
+            if (!err) err = done_wait(c, (const int *)c->dscratch, c->cache_swaponly ? 0 : nseg, stream);
             if (!err && c->timing) batch_time(c);
             if (!err)
                 for (i = 0; i < nseg; i++)
-                    hstat[i] = !c->cache_swaponly && ((int *)c->hscratch)[i] == sval ? NC_ERANGE : NC_NOERR;
+                    hstat[i] = !c->cache_swaponly && c->hdone_h[16 + i] == sval ? NC_ERANGE : NC_NOERR;
         }
         pthread_mutex_unlock(&c->lock);
         goto out;
@@ -1498,15 +1533,13 @@ static int dev_batch(const pncx_seg *segs, int nseg, int *status_out, int *dstat
         if (async) {
             if (!err) { c->async_pending = 1; c->async_stream = stream; }
         } else {
-            /* statuses land in the pinned mirror's status area (zeroed by the
-             * upload); a batch of swaps and copies only has nothing to read */
-            if (!err && !swaponly)
-                err = pncxrt_memcpy_d2h(c->hscratch, c->dscratch, sizeof(int) * (size_t)nseg, stream);
-            if (!err) err = spin_wait(c, stream);
+            /* the status words were zeroed by the upload; a batch of swaps
+             * and copies only has nothing to read */
+            if (!err) err = done_wait(c, (const int *)c->dscratch, swaponly ? 0 : nseg, stream);
             if (!err && c->timing) batch_time(c);
             if (!err && !swaponly)
                 for (i = 0; i < nseg; i++)
-                    if (hstat[i] == NC_NOERR) hstat[i] = ((int *)c->hscratch)[i] != 0 ? NC_ERANGE : NC_NOERR;
+                    if (hstat[i] == NC_NOERR) hstat[i] = c->hdone_h[16 + i] != 0 ? NC_ERANGE : NC_NOERR;
         }
         /* keep the plan when every segment runs in a class kernel */
         c->cache_valid = 0;
@@ -1560,14 +1593,17 @@ int pncx_dev_batch_timing(int enable)
     ctx_t *c;
     if (!have_device() || (c = get_ctx()) == NULL) return PNCX_EDEVICE;
     pthread_mutex_lock(&c->lock);
-    if (enable && c->tev0 == NULL &&
-        (pncxrt_event_create(&c->tev0) != 0 || pncxrt_event_create(&c->tev1) != 0)) {
-        pncxrt_event_destroy(c->tev0);
-        c->tev0 = c->tev1 = NULL;
-        pthread_mutex_unlock(&c->lock);
-        return PNCX_EDEVICE;
+    if (enable && c->tev[2 * NTEV - 1] == NULL) {
+        int k;
+        for (k = 0; k < 2 * NTEV; k++)
+            if (c->tev[k] == NULL && pncxrt_event_create(&c->tev[k]) != 0) {
+                c->tev[k] = NULL;
+                pthread_mutex_unlock(&c->lock);
+                return PNCX_EDEVICE;
+            }
     }
     c->timing = enable != 0;
+    c->tpend = 0;
     c->tms = 0.0;
     c->tcalls = 0;
     pthread_mutex_unlock(&c->lock);
@@ -1582,6 +1618,7 @@ int pncx_dev_batch_kernel_ms(double *total_ms, long long *calls)
     *calls = 0;
     if (!have_device() || (c = get_ctx()) == NULL) return PNCX_EDEVICE;
     pthread_mutex_lock(&c->lock);
+    batch_time_drain(c);
     *total_ms = c->tms;
     *calls = c->tcalls;
     pthread_mutex_unlock(&c->lock);

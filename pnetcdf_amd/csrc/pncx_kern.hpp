@@ -18,6 +18,8 @@
 #include "pncx_device.hpp"
 #include "pncx_shim.h"
 
+#include <hip/hip_ext.h>
+
 namespace pncx {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -231,7 +233,8 @@ __device__ __forceinline__ void publish(const Sink &s, int *status, bool bad) {
 // the launcher side (pncx_kern_swap.hip)
 Sink sink_acquire(int *status, int sval, hipStream_t st, int64_t nblocks, bool want);
 int sink_finish(const Sink &s, hipStream_t st, int64_t nblocks, int err);
-int sink_finish_batch(const Sink &s, const pncxk_seg *dsegs, int nseg, int64_t nblocks, hipStream_t st, int err);
+int sink_finish_batch(const Sink &s, const pncxk_seg *dsegs, int nseg, int64_t nblocks, hipStream_t st, int err,
+                      hipEvent_t ev_stop = nullptr);
 
 // can a conversion from S to D report NC_ERANGE at all (get1/put1 rules):
 // into a floating type only double -> float is checked; from a floating type
@@ -945,9 +948,16 @@ int launch_batch(const pncxk_batch_args *a) {
     if constexpr (Op::PRESERVE) return NC_EINVAL;   // host runs these one by one
     hipStream_t st = (hipStream_t)a->stream;
     const Sink sk = sink_acquire(nullptr, a->sval, st, a->nblocks, may_range<Op>::value);
-    hipLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0, st, a->dsegs, a->nseg,
-                       a->uniform, a->dmap, a->grp, sk);
-    return sink_finish_batch(sk, a->dsegs, a->nseg, a->nblocks, st, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
+    // timing: the stop event goes on the flag reduce when there is one
+    hipEvent_t e0 = (hipEvent_t)a->ev_start, e1 = (hipEvent_t)a->ev_stop;
+    if (e0 != nullptr || e1 != nullptr)
+        hipExtLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0, st, e0,
+                              sk.flags != nullptr ? nullptr : e1, 0, a->dsegs, a->nseg, a->uniform, a->dmap, a->grp, sk);
+    else
+        hipLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0, st, a->dsegs, a->nseg,
+                           a->uniform, a->dmap, a->grp, sk);
+    return sink_finish_batch(sk, a->dsegs, a->nseg, a->nblocks, st, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE,
+                             sk.flags != nullptr ? e1 : nullptr);
 }
 
 template <class Op>

@@ -270,11 +270,16 @@ int sink_finish(const Sink &s, hipStream_t st, int64_t nblocks, int err) {
     return err;
 }
 
-int sink_finish_batch(const Sink &s, const pncxk_seg *dsegs, int nseg, int64_t nblocks, hipStream_t st, int err) {
+int sink_finish_batch(const Sink &s, const pncxk_seg *dsegs, int nseg, int64_t nblocks, hipStream_t st, int err,
+                      hipEvent_t ev_stop) {
     if (s.flags == nullptr) return err;
     if (!err && nseg > 0) {
-        hipLaunchKernelGGL(k_flags_batch, dim3((unsigned)nseg), dim3(256), 0, st, dsegs, nseg, nblocks, s.flags,
-                           s.epoch, s.sval);
+        if (ev_stop != nullptr)
+            hipExtLaunchKernelGGL(k_flags_batch, dim3((unsigned)nseg), dim3(256), 0, st, nullptr, ev_stop, 0, dsegs,
+                                  nseg, nblocks, (const int *)s.flags, s.epoch, s.sval);
+        else
+            hipLaunchKernelGGL(k_flags_batch, dim3((unsigned)nseg), dim3(256), 0, st, dsegs, nseg, nblocks, s.flags,
+                               s.epoch, s.sval);
         if (hipGetLastError() != hipSuccess) err = PNCX_EDEVICE;
     }
     sink_release(st);
@@ -349,9 +354,14 @@ __global__ __launch_bounds__(MIX_LANES) void k_batch_swapmix(const pncxk_seg *se
 extern "C" int pncxk_batch(int kind, int a, int b, int c, const pncxk_batch_args *args) {
     if (kind == PNCXK_SWAPMIX) {
         if (args->nblocks <= 0) return 0;
-        hipLaunchKernelGGL(k_batch_swapmix, dim3((unsigned)args->nblocks), dim3(MIX_LANES), 0,
-                           (hipStream_t)args->stream, args->dsegs, args->nseg, args->uniform, args->dmap,
-                           args->grp);
+        if (args->ev_start != nullptr || args->ev_stop != nullptr)
+            hipExtLaunchKernelGGL(k_batch_swapmix, dim3((unsigned)args->nblocks), dim3(MIX_LANES), 0,
+                                  (hipStream_t)args->stream, (hipEvent_t)args->ev_start, (hipEvent_t)args->ev_stop, 0,
+                                  args->dsegs, args->nseg, args->uniform, args->dmap, args->grp);
+        else
+            hipLaunchKernelGGL(k_batch_swapmix, dim3((unsigned)args->nblocks), dim3(MIX_LANES), 0,
+                               (hipStream_t)args->stream, args->dsegs, args->nseg, args->uniform, args->dmap,
+                               args->grp);
         return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
     }
     if (kind == PNCXK_SWAP) {
@@ -405,6 +415,26 @@ extern "C" int pncxk_batch_map(const pncxk_batch_args *a) {
     return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
 }
 
+// Completion of a synchronous pncx_dev_batch: the statuses go straight into
+// host-mapped (fine-grained) memory and a sequence word follows them, which
+// the host polls -- no status copy command and no completion event.  A
+// 768 MiB swap kernel waited for this way took 257 us per call against 260
+// with hipEventRecord + hipEventQuery and 248 back to back
+// (tools/turnaround_probe.hip, profiles/r02_turnaround_probe.txt).  One
+// block; vector stores only.
+__global__ __launch_bounds__(256) void k_batch_done(const int *dstat, int n, int *hstat, int *hdone, int seq) {
+    for (int i = threadIdx.x; i < n; i += 256) __hip_atomic_store(hstat + i, dstat[i], __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(hdone, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+extern "C" int pncxk_batch_done(const int *dstat, int n, int *hstat, int *hdone, int seq, void *stream) {
+    hipLaunchKernelGGL(k_batch_done, dim3(1), dim3(256), 0, (hipStream_t)stream, dstat, n, hstat, hdone, seq);
+    return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
+}
+
 extern "C" int pncxk_opinfo_get(int kind, int a, int b, int c, pncxk_opinfo *o) {
     if (kind == PNCXK_SWAP) {
         switch (a) {
@@ -446,6 +476,17 @@ int pncxrt_malloc(void **p, size_t n) { return rt(hipMalloc(p, n ? n : 1), "hipM
 int pncxrt_free(void *p) { return p ? rt(hipFree(p), "hipFree") : 0; }
 int pncxrt_host_alloc(void **p, size_t n) {
     return rt(hipHostMalloc(p, n ? n : 1, hipHostMallocDefault), "hipHostMalloc");
+}
+int pncxrt_host_alloc_mapped(void **p, void **dp, size_t n) {
+    *p = *dp = nullptr;
+    if (rt(hipHostMalloc(p, n ? n : 1, hipHostMallocCoherent | hipHostMallocMapped), "hipHostMalloc coherent"))
+        return PNCX_EDEVICE;
+    if (rt(hipHostGetDevicePointer(dp, *p, 0), "hipHostGetDevicePointer")) {
+        (void)hipHostFree(*p);
+        *p = *dp = nullptr;
+        return PNCX_EDEVICE;
+    }
+    return 0;
 }
 int pncxrt_host_free(void *p) { return p ? rt(hipHostFree(p), "hipHostFree") : 0; }
 int pncxrt_memcpy_h2d(void *d, const void *h, size_t n, void *s) {

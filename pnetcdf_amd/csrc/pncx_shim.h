@@ -55,6 +55,8 @@ typedef struct pncxk_batch_args {
     pncxk_groups     grp;      /* used when uniform == 0 and grp.n > 0     */
     int              sval;     /* value a segment's status word gets on ERANGE */
     void            *stream;
+    void            *ev_start; /* timing events stamped at this launch's start */
+    void            *ev_stop;  /* and end (hipExtLaunchKernel), or NULL      */
 } pncxk_batch_args;
 
 /* varm layout of the user buffer (create_imaptype.c semantics) */
@@ -119,6 +121,9 @@ int pncxk_first_diff(const void *a, const void *b, long long n, int itype, int t
                      unsigned long long *first, void *stream);
 /* fill args->dmap (nblocks ints) from the device descriptors */
 int pncxk_batch_map(const pncxk_batch_args *args);
+/* completion of a synchronous batch: copy n status words to host-mapped
+ * hstat, then store seq into host-mapped *hdone (system scope) */
+int pncxk_batch_done(const int *dstat, int n, int *hstat, int *hdone, int seq, void *stream);
 
 /* ---- HIP runtime wrappers (return 0 on success, PNCX_EDEVICE on error) ---- */
 int  pncxrt_device_count(void);
@@ -127,6 +132,9 @@ int  pncxrt_get_device(void);
 int  pncxrt_malloc(void **p, size_t n);
 int  pncxrt_free(void *p);
 int  pncxrt_host_alloc(void **p, size_t n);
+/* fine-grained (coherent) pinned memory the device writes directly: *dp is
+ * the device-side address of *p */
+int  pncxrt_host_alloc_mapped(void **p, void **dp, size_t n);
 int  pncxrt_host_free(void *p);
 int  pncxrt_memcpy_h2d(void *d, const void *h, size_t n, void *stream);
 int  pncxrt_memcpy_d2h(void *h, const void *d, size_t n, void *stream);

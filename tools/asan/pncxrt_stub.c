@@ -15,6 +15,7 @@ int pncxrt_get_device(void) { return 0; }
 int pncxrt_malloc(void **p, size_t n) { (void)p; (void)n; return NODEV; }
 int pncxrt_free(void *p) { (void)p; return 0; }
 int pncxrt_host_alloc(void **p, size_t n) { (void)p; (void)n; return NODEV; }
+int pncxrt_host_alloc_mapped(void **p, void **dp, size_t n) { (void)p; (void)dp; (void)n; return NODEV; }
 int pncxrt_host_free(void *p) { (void)p; return 0; }
 int pncxrt_memcpy_h2d(void *d, const void *h, size_t n, void *s) { (void)d; (void)h; (void)n; (void)s; return NODEV; }
 int pncxrt_memcpy_d2h(void *h, const void *d, size_t n, void *s) { (void)d; (void)h; (void)n; (void)s; return NODEV; }
@@ -44,6 +45,7 @@ int pncxk_launch_imap(int k, int a, int b, int c, const pncxk_args *x, const pnc
 int pncxk_opinfo_get(int k, int a, int b, int c, pncxk_opinfo *o) { (void)k; (void)a; (void)b; (void)c; (void)o; return NODEV; }
 int pncxk_fill(void *d, long long n, int x, const void *v, void *s) { (void)d; (void)n; (void)x; (void)v; (void)s; return NODEV; }
 int pncxk_batch_map(const pncxk_batch_args *x) { (void)x; return NODEV; }
+int pncxk_batch_done(const int *d, int n, int *h, int *w, int q, void *s) { (void)d; (void)n; (void)h; (void)w; (void)q; (void)s; return NODEV; }
 int pncxk_first_diff(const void *a, const void *b, long long n, int t, int tol, double td, double tr,
                      unsigned long long *f, void *s)
 { (void)a; (void)b; (void)n; (void)t; (void)tol; (void)td; (void)tr; (void)f; (void)s; return NODEV; }
