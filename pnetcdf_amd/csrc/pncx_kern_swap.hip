@@ -303,6 +303,12 @@ constexpr int MIX_LANES = PNCXK_MIX_LANES;
 // 77-87 % of HBM peak depending on where the buffers were placed, against
 // 81-83 % for one contiguous buffer of the same bytes (tools/batch_sweep.hip,
 // profiles/r01_batch_sweep*.txt).  1024 lanes = 4x fewer blocks to schedule.
+// Round 2, in this kernel and one process (tools/c4_placement.py,
+// profiles/r02_c4_placement*.jsonl): one allocation per buffer, torch
+// sub-allocations, one pool and two flat segments all run at 77-79 % of
+// peak, so placement does not explain the gap; plain (write-back) stores
+// lose 1-4 points to "nt sc1" on every placement.  Persistent grids that
+// prefetch their next tile ran at 65-74 % (tools/c4_store_sweep.hip).
 __device__ __forceinline__ u32x4 swap16(u32x4 v, int es) {
     u32x4 r = v;
     if (es == 2) {
@@ -354,12 +360,13 @@ __global__ __launch_bounds__(MIX_LANES) void k_batch_swapmix(const pncxk_seg *se
 extern "C" int pncxk_batch(int kind, int a, int b, int c, const pncxk_batch_args *args) {
     if (kind == PNCXK_SWAPMIX) {
         if (args->nblocks <= 0) return 0;
+        auto k = k_batch_swapmix;
         if (args->ev_start != nullptr || args->ev_stop != nullptr)
-            hipExtLaunchKernelGGL(k_batch_swapmix, dim3((unsigned)args->nblocks), dim3(MIX_LANES), 0,
+            hipExtLaunchKernelGGL(k, dim3((unsigned)args->nblocks), dim3(MIX_LANES), 0,
                                   (hipStream_t)args->stream, (hipEvent_t)args->ev_start, (hipEvent_t)args->ev_stop, 0,
                                   args->dsegs, args->nseg, args->uniform, args->dmap, args->grp);
         else
-            hipLaunchKernelGGL(k_batch_swapmix, dim3((unsigned)args->nblocks), dim3(MIX_LANES), 0,
+            hipLaunchKernelGGL(k, dim3((unsigned)args->nblocks), dim3(MIX_LANES), 0,
                                (hipStream_t)args->stream, args->dsegs, args->nseg, args->uniform, args->dmap,
                                args->grp);
         return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;

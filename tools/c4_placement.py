@@ -98,14 +98,16 @@ def main():
                         seg(T.NC_FLOAT, T.ITYPE_FLOAT, h, xpool.data_ptr() + 2 * h, ipool.data_ptr() + 2 * h)]
     if a.only:
         layouts = {a.only: layouts[a.only]}
-    arrs = {k: (pncx.Seg * len(v))(*v) for k, v in layouts.items()}
+    arrs = {}
+    for k, v in layouts.items():       # (plain stores were compared through a since-removed switch)
+        arrs[(k, "nt_sc1")] = (pncx.Seg * len(v))(*v)
     dst = torch.zeros(NVAR, dtype=torch.int32, device="cuda")
     dp = ctypes.c_void_p(dst.data_ptr())
     moved = NVAR // 2 * NEL * (2 + 2 + 4 + 4)
     res = {k: [] for k in arrs}
     torch.cuda.synchronize()
     for r in range(a.rounds + 1):
-        for k, arr in arrs.items():
+        for (k, pol), arr in arrs.items():
             for _ in range(3):
                 assert lib.pncx_dev_batch_async(arr, len(arr), dp, sp) == 0
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
@@ -115,10 +117,10 @@ def main():
                 e1.record(stream)
             torch.cuda.synchronize()
             if r > 0:
-                res[k] += [e0.elapsed_time(e1) for e0, e1 in ev]
+                res[(k, pol)] += [e0.elapsed_time(e1) for e0, e1 in ev]
     for k, v in res.items():
         med, best = statistics.median(v), min(v)
-        print(json.dumps({"layout": k, "median_ms": round(med, 4), "best_ms": round(best, 4),
+        print(json.dumps({"layout": k[0], "store": k[1], "median_ms": round(med, 4), "best_ms": round(best, 4),
                           "median_GBps": round(moved / med / 1e6, 1), "frac_median": round(moved / med / 8e9, 4),
                           "frac_best": round(moved / best / 8e9, 4), "launches": len(v)}), flush=True)
 

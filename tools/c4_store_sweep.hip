@@ -5,7 +5,11 @@
 // group rule of k_batch_swapmix), 1024 lanes x 16 B per block, with
 //   loads:  nt (nontemporal builtin) | plain
 //   stores: nt | nt sc1 (inline asm) | plain
-// Launches queued back to back (20 per sample); interleaved rounds.
+// plus persistent blocks that prefetch their next tile (all 65-74 %:
+// profiles/r02_c4_store_sweep.txt).  Launches queued back to back (20 per
+// sample); interleaved rounds.  Sources hold splitmix64 bits: with memset
+// patterns (round 1's sweeps) plain stores looked best, with random bits
+// they lose (the product's bench inputs are random).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -60,12 +64,61 @@ __global__ __launch_bounds__(1024) void k_seg(const Seg *segs) {
     st<ST>(sg.dst + i, sw(ld<LD>(sg.src + i), sg.es));
 }
 
+// persistent blocks with the next tile's load issued before the current
+// tile's store (one 16 B vector per lane per tile, BS-lane tiles); tiles
+// dealt round-robin over the grid (block k takes tiles k, k + grid, ...)
+template <int BS, bool SEG>
+__global__ __launch_bounds__(BS) void k_persist(const Seg *segs, const u32x4 *fsrc, u32x4 *fdst, long long ntile) {
+    constexpr long long T2 = 2048 / BS * 128, T4 = 4096 / BS * 128;   // tiles per short / float buffer... per segment
+    auto addr = [&](long long t, const u32x4 *&s, u32x4 *&d, int &es) {
+        if constexpr (SEG) {
+            const long long per_s = 2ll * (1 << 20) / (BS * 16), per_f = 4ll * (1 << 20) / (BS * 16);
+            int k;
+            long long rel;
+            if (t < 128 * per_s) { k = (int)(t / per_s); rel = t - k * per_s; }
+            else { const long long u = t - 128 * per_s; k = 128 + (int)(u / per_f); rel = u - (k - 128) * per_f; }
+            s = segs[k].src + rel * BS + threadIdx.x;
+            d = segs[k].dst + rel * BS + threadIdx.x;
+            es = segs[k].es;
+        } else {
+            s = fsrc + t * BS + threadIdx.x;
+            d = fdst + t * BS + threadIdx.x;
+            es = 4;
+        }
+    };
+    (void)T2; (void)T4;
+    long long t = blockIdx.x;
+    if (t >= ntile) return;
+    const u32x4 *s; u32x4 *d; int es;
+    addr(t, s, d, es);
+    u32x4 v = __builtin_nontemporal_load(s);
+    for (;;) {
+        const long long tn = t + gridDim.x;
+        const u32x4 *s2 = nullptr; u32x4 *d2 = nullptr; int es2 = 4;
+        u32x4 v2;
+        const bool more = tn < ntile;
+        if (more) { addr(tn, s2, d2, es2); v2 = __builtin_nontemporal_load(s2); }
+        st<1>(d, sw(v, es));
+        if (!more) break;
+        t = tn; d = d2; es = es2; v = v2;
+    }
+}
+
+__global__ void k_rand(uint64_t *p, long long n, uint64_t seed) {
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        uint64_t z = seed + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
 int main() {
     const long long total = 768ll << 20, nb = total / (1024 * 16);
     u32x4 *fs, *fd;
     CK(hipMalloc(&fs, total));
     CK(hipMalloc(&fd, total));
-    CK(hipMemset(fs, 0x3c, total));
+    k_rand<<<4096, 256>>>((uint64_t *)fs, total / 8, 1);
     std::vector<Seg> h(256);
     long long b0 = 0;
     for (int s = 0; s < 256; s++) {
@@ -74,7 +127,7 @@ int main() {
         u32x4 *a, *d;
         CK(hipMalloc(&a, bytes));
         CK(hipMalloc(&d, bytes));
-        CK(hipMemset(a, 0x3c, bytes));
+        k_rand<<<1024, 256>>>((uint64_t *)a, (long long)bytes / 8, 100 + s);
         h[s] = {a, d, b0, es, 0};
         b0 += bytes / (1024 * 16);
     }
@@ -88,8 +141,11 @@ int main() {
         [](const Seg *, u32x4 *a, u32x4 *d, long long n) { k_flat<L, S><<<n, 1024>>>(a, d); }, {}});
 #define SG(L, S) vs.push_back({std::string("seg  ld") + (L ? "plain" : "nt") + " st" + (S == 0 ? "nt" : S == 1 ? "nt_sc1" : "plain"), \
         [](const Seg *s, u32x4 *, u32x4 *, long long n) { k_seg<L, S><<<n, 1024>>>(s); }, {}});
-    FL(0, 0) FL(0, 1) FL(0, 2) FL(1, 0) FL(1, 1) FL(1, 2)
-    SG(0, 0) SG(0, 1) SG(0, 2) SG(1, 0) SG(1, 1) SG(1, 2)
+    FL(0, 0) FL(0, 1) FL(0, 2) SG(0, 0) SG(0, 1) SG(0, 2) SG(1, 1)
+#define PS(BS, SEGM, OCC) vs.push_back({std::string("persist bs") + #BS + (SEGM ? " seg" : " flat") + " occ" + #OCC, \
+        [](const Seg *s, u32x4 *a, u32x4 *d, long long n) { \
+            k_persist<BS, SEGM><<<256 * OCC, BS>>>(s, a, d, n * 1024 / BS); }, {}});
+    PS(256, true, 8)
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
