@@ -175,7 +175,10 @@ int main(int argc, char **argv) {
     add("current 64x64 v1/v1 bs256", [=] { hipLaunchKernelGGL(k_cur, dim3(n / 4096), dim3(256), 0, 0, user, ref, g); });
 #define TR(TP, TU, VU, VP, BS) add(std::string("tile ") + #TP "x" #TU " vu" #VU " vp" #VP " bs" #BS, [=] { \
         hipLaunchKernelGGL((k_tr<TP, TU, VU, VP, BS>), dim3(n / (TP * TU)), dim3(BS), 0, 0, user, packed, g); });
-    TR(64, 64, 1, 1, 256)
+    TR(64, 64, 1, 1, 256) TR(64, 64, 2, 2, 256)
+    // longer contiguous runs per row / column (round 2)
+    TR(64, 128, 1, 1, 256) TR(64, 128, 2, 1, 256) TR(64, 128, 2, 2, 256) TR(128, 64, 1, 2, 256)
+    TR(128, 64, 2, 2, 256) TR(128, 128, 2, 2, 512) TR(64, 256, 2, 1, 512) TR(64, 256, 2, 2, 512)
     {
         G2 g2 = {g.c0 / 64, g.c2 / 64, n / 4096, g.c1 * g.c2, g.c2, g.c0, g.c0 * g.c1};
 #define TR2(F) add(std::string("ablation flags ") + #F, [=] { hipLaunchKernelGGL((k_tr2<F>), dim3(n / 4096), dim3(256), 0, 0, user, packed, g2); });
@@ -193,7 +196,7 @@ int main(int argc, char **argv) {
         const unsigned grid = (unsigned)tg.ntiles;
         add("product k_imap_tile (aligned)", [=] {
             hipLaunchKernelGGL((pncx::k_imap_tile<pncx::SwapOp<8>, true, true>), dim3(grid), dim3(256), 0, 0,
-                               (const uint8_t *)user, (uint8_t *)packed, tg, 0ULL, (int *)nullptr); });
+                               (const uint8_t *)user, (uint8_t *)packed, tg, 0ULL, pncx::Sink{nullptr, nullptr, 0, 0}); });
     }
     add("flat swap copy (same bytes)", [=] { hipLaunchKernelGGL(k_copy, dim3(n / 2 / 256), dim3(256), 0, 0,
                                                                   (const u64x2 *)user, (u64x2 *)packed, n / 2); });
@@ -217,15 +220,20 @@ int main(int argc, char **argv) {
         CK(hipMemcpy(hp.data(), packed, n * 8, hipMemcpyDeviceToHost));
         if (hp != hr) printf("MISMATCH: %s\n", vars[k].name.c_str());
     }
+    // each sample: one warm launch, then 10 launches of the same kernel back
+    // to back between the events (round 1 timed single launches after a
+    // different kernel, and the order then moved results by ~10 points:
+    // the 256 MiB sides are the size of the Infinity Cache)
     for (int r = 0; r < rounds; r++)
         for (auto &v : vars) {
-            CK(hipEventRecord(a, 0));
             v.run();
+            CK(hipEventRecord(a, 0));
+            for (int k = 0; k < 10; k++) v.run();
             CK(hipEventRecord(b, 0));
             CK(hipEventSynchronize(b));
             float ms;
             CK(hipEventElapsedTime(&ms, a, b));
-            v.ms.push_back(ms);
+            v.ms.push_back(ms / 10);
         }
     CK(hipGetLastError());
     const double moved = 16.0 * n;
