@@ -640,11 +640,17 @@ __global__ __launch_bounds__(256) void k_tmap_runs(const uint8_t *src, uint8_t *
 // ---------------------------------------------------------------------------
 // varm transpose: when the user buffer's fastest dimension U (smallest imap)
 // is not the packed order's fastest dimension P (the last), per-element
-// gathers touch one cache line per lane.  A 64 x 64 tile of (P, U) goes
-// through LDS instead: read coalesced along U in the user buffer, write
-// coalesced along P in the packed buffer (put); the reverse for get.  Other
-// dimensions index the tile grid.  The conversion runs on the packed side.
+// gathers touch one cache line per lane.  A tile of XT_P x XT_U elements of
+// (P, U) goes through LDS instead: read coalesced along U in the user buffer,
+// write coalesced along P in the packed buffer (put); the reverse for get.
+// Other dimensions index the tile grid.  The conversion runs on the packed
+// side.  XT_U = 128: a user row is read as one 1 KiB run (doubles) instead of
+// 512 B; 64 x 128 ran at 69 % of peak against 62-64 % for 64 x 64 on the
+// 512 x 512 x 128 double transpose and 72.5 against 71 % at 1024 x 1024 x 128
+// (tools/transpose_sweep.hip, profiles/r02_transpose_sweep_wide_tiles.txt).
 // ---------------------------------------------------------------------------
+constexpr int XT_P = 64, XT_U = 128;
+
 struct TransposeGeom {
     int64_t cp, cu;          // count[P], count[U]
     int64_t ip, iu;          // imap[P], imap[U] (user elements)
@@ -657,85 +663,127 @@ struct TransposeGeom {
 
 template <typename T>
 __device__ __forceinline__ T ld_nt(const uint8_t *p) { return __builtin_nontemporal_load(reinterpret_cast<const T *>(p)); }
-template <typename T>
-__device__ __forceinline__ void st_nt(uint8_t *p, T v) { st_stream<T>(p, v); }
+template <typename T, bool SC1 = true>
+__device__ __forceinline__ void st_nt(uint8_t *p, T v) {
+    if constexpr (SC1) st_stream<T>(p, v);
+    else __builtin_nontemporal_store(v, reinterpret_cast<T *>(p));
+}
 
-// One 64 x 64 tile, both buffers element-aligned: the 16 loads per lane go
-// out before anything is stored, with nontemporal global accesses, and per-
-// lane addresses advance by a fixed row / column stride.  FULL tiles need no
-// bounds; in a partial tile the load indices are clamped into the tile, so
-// the extra lanes re-read (and convert) valid elements and only the stores
-// are predicated -- a predicated load costs a wait of its own (5.0 -> 4.0
-// TB/s measured).
-template <class Op, bool GATHER, bool FULL, typename TU>
+// One tile, both buffers element-aligned.  256 threads: on the user side a
+// row of XT_U elements is 128 lanes (2 rows per pass, 32 passes), on the
+// packed side a column of XT_P elements is 64 lanes (4 columns per pass, 32
+// passes).  All 32 loads per lane go out before anything is stored, with
+// nontemporal global accesses, and per-lane addresses advance by a fixed
+// row / column stride.  FULL tiles need no bounds; in a partial tile the load
+// indices are clamped into the tile, so the extra lanes re-read (and
+// convert) valid elements and only the stores are predicated -- a predicated
+// load costs a wait of its own (5.0 -> 4.0 TB/s measured).
+template <class Op, bool GATHER, bool FULL, typename TU, bool SC1>
 __device__ __forceinline__ void xpose_tile(const uint8_t *src, uint8_t *dst, const TransposeGeom &g, int64_t pbase,
                                            int64_t ubase, int64_t p0, int64_t u0, int np, int nu,
-                                           TU (*tile)[65], typename Op::fill_t fill, bool &bad) {
+                                           TU (*tile)[XT_U + 1], typename Op::fill_t fill, bool &bad) {
     using SU = typename Op::SU;
     using DU = typename Op::DU;
     constexpr int UES = GATHER ? Op::SS : Op::DS;
     constexpr int PES = GATHER ? Op::DS : Op::SS;
-    const int lo6 = threadIdx.x & 63, hi2 = threadIdx.x >> 6;
+    constexpr int RPP = 256 / XT_U, NR = XT_P / RPP;      // user side: rows per pass, passes
+    constexpr int CPP = 256 / XT_P, NC = XT_U / CPP;      // packed side: columns per pass, passes
+    const int lu = threadIdx.x % XT_U, ru = threadIdx.x / XT_U;     // user-side lane, row
+    const int lp = threadIdx.x % XT_P, cp = threadIdx.x / XT_P;     // packed-side lane, column
     const int64_t rs = g.ip * UES, cs = g.su * PES;        // bytes between rows p (user), columns u (packed)
     if constexpr (GATHER) {
-        const int cl = FULL || lo6 < nu ? lo6 : nu - 1;
+        const int cl = FULL || lu < nu ? lu : nu - 1;
         const uint8_t *s0 = src + (ubase + p0 * g.ip + (u0 + cl) * g.iu) * UES;
-        TU v[16];
+        TU v[NR];
+        if constexpr (FULL) {
+            // one running address: 32 precomputed 64-bit addresses would cost
+            // 64 VGPRs on top of the 64 the data takes
+            const uint8_t *sp = s0 + ru * rs;
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const int r = FULL || hi2 + 4 * i < np ? hi2 + 4 * i : np - 1;
-            v[i] = ld_nt<TU>(s0 + r * rs);
+            for (int i = 0; i < NR; i++, sp += RPP * rs) v[i] = ld_nt<TU>(sp);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NR; i++) {
+                const int r = ru + RPP * i < np ? ru + RPP * i : np - 1;
+                v[i] = ld_nt<TU>(s0 + r * rs);
+            }
         }
 #pragma unroll
-        for (int i = 0; i < 16; i++) tile[hi2 + 4 * i][lo6] = v[i];
+        for (int i = 0; i < NR; i++) tile[ru + RPP * i][lu] = v[i];
         __syncthreads();
-        uint8_t *d0 = dst + (pbase + u0 * g.su + p0 + lo6) * PES;
-        DU o[16];
+        uint8_t *d0 = dst + (pbase + u0 * g.su + p0 + lp) * PES;
+        DU o[NC];
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
+        for (int i = 0; i < NC; i++) {
             DU old = 0;
             if constexpr (Op::PRESERVE)
-                if (FULL || (hi2 + 4 * i < nu && lo6 < np)) old = ld_unaligned<DU>(d0 + (hi2 + 4 * i) * cs);
-            o[i] = Op::one(tile[lo6][hi2 + 4 * i], old, fill, bad);
+                if (FULL || (cp + CPP * i < nu && lp < np)) old = ld_unaligned<DU>(d0 + (cp + CPP * i) * cs);
+            o[i] = Op::one(tile[lp][cp + CPP * i], old, fill, bad);
         }
+        if constexpr (FULL) {
+            uint8_t *dp = d0 + cp * cs;
 #pragma unroll
-        for (int i = 0; i < 16; i++)
-            if (FULL || (hi2 + 4 * i < nu && lo6 < np)) st_nt<DU>(d0 + (hi2 + 4 * i) * cs, o[i]);
+            for (int i = 0; i < NC; i++, dp += CPP * cs) st_nt<DU, SC1>(dp, o[i]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NC; i++)
+                if (cp + CPP * i < nu && lp < np) st_nt<DU, SC1>(d0 + (cp + CPP * i) * cs, o[i]);
+        }
     } else {
-        const int pl = FULL || lo6 < np ? lo6 : np - 1;
+        const int pl = FULL || lp < np ? lp : np - 1;
         const uint8_t *s0 = src + (pbase + u0 * g.su + p0 + pl) * PES;
-        SU v[16];
+        SU v[NC];
+        if constexpr (FULL) {
+            const uint8_t *sp = s0 + cp * cs;
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const int c = FULL || hi2 + 4 * i < nu ? hi2 + 4 * i : nu - 1;
-            v[i] = ld_nt<SU>(s0 + c * cs);
+            for (int i = 0; i < NC; i++, sp += CPP * cs) v[i] = ld_nt<SU>(sp);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NC; i++) {
+                const int c = cp + CPP * i < nu ? cp + CPP * i : nu - 1;
+                v[i] = ld_nt<SU>(s0 + c * cs);
+            }
         }
         // clamped duplicates convert like the element they copy: no false NC_ERANGE
 #pragma unroll
-        for (int i = 0; i < 16; i++) tile[lo6][hi2 + 4 * i] = Op::one(v[i], DU(0), fill, bad);
+        for (int i = 0; i < NC; i++) tile[lp][cp + CPP * i] = Op::one(v[i], DU(0), fill, bad);
         __syncthreads();
-        uint8_t *d0 = dst + (ubase + p0 * g.ip + (u0 + lo6) * g.iu) * UES;
-        TU o[16];
+        uint8_t *d0 = dst + (ubase + p0 * g.ip + (u0 + lu) * g.iu) * UES;
+        TU o[NR];
 #pragma unroll
-        for (int i = 0; i < 16; i++) o[i] = tile[hi2 + 4 * i][lo6];
+        for (int i = 0; i < NR; i++) o[i] = tile[ru + RPP * i][lu];
+        if constexpr (FULL) {
+            uint8_t *dp = d0 + ru * rs;
 #pragma unroll
-        for (int i = 0; i < 16; i++)
-            if (FULL || (hi2 + 4 * i < np && lo6 < nu)) st_nt<TU>(d0 + (hi2 + 4 * i) * rs, o[i]);
+            for (int i = 0; i < NR; i++, dp += RPP * rs) st_nt<TU, SC1>(dp, o[i]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NR; i++)
+                if (ru + RPP * i < np && lu < nu) st_nt<TU, SC1>(d0 + (ru + RPP * i) * rs, o[i]);
+        }
     }
 }
 
 // ALIGNED: both buffers element-aligned (checked at launch): xpose_tile.
 // Otherwise the bounds-checked loops below with unaligned accesses.
-template <class Op, bool GATHER, bool ALIGNED>
-__global__ __launch_bounds__(256) void k_imap_tile(const uint8_t *src, uint8_t *dst, TransposeGeom g,
+// (256, 2): at least 2 waves per SIMD, i.e. two blocks per CU, which the
+// 66 KiB tile allows -- unconstrained the 32 loads in flight per lane took
+// 268 VGPRs and left one block per CU (56 % of peak instead of 68 %)
+// SC1 = false: plain nontemporal stores -- unlike the streaming sweeps, the
+// transpose runs 2 points faster without write-through (65.9 against 63.7 %
+// of peak, profiles/r02_transpose_sweep_product.txt)
+template <class Op, bool GATHER, bool ALIGNED, bool SC1 = false>
+__global__ __launch_bounds__(256, 2) void k_imap_tile(const uint8_t *src, uint8_t *dst, TransposeGeom g,
                                                    typename Op::fill_t fill, Sink sk) {
     using SU = typename Op::SU;
     using DU = typename Op::DU;
     using TU = typename std::conditional<GATHER, SU, DU>::type;     // LDS holds user-side bits
     constexpr int UES = GATHER ? Op::SS : Op::DS;
     constexpr int PES = GATHER ? Op::DS : Op::SS;
-    __shared__ TU tile[64][65];
-    const int t = threadIdx.x, lo6 = t & 63, hi2 = t >> 6;
+    __shared__ TU tile[XT_P][XT_U + 1];
+    const int t = threadIdx.x;
+    const int lu = t % XT_U, ru = t / XT_U, lp = t % XT_P, cp = t / XT_P;
+    constexpr int RPP = 256 / XT_U, CPP = 256 / XT_P;
     bool bad = false;
     const bool small = g.ntiles < (1LL << 32);          // tile decode in 32 bits (scalar divisions)
     for (int64_t b = xcd_remap(blockIdx.x, gridDim.x); b < g.ntiles; b += gridDim.x) {
@@ -765,37 +813,37 @@ __global__ __launch_bounds__(256) void k_imap_tile(const uint8_t *src, uint8_t *
                 ubase += i * g.ostride_u[d];
             }
         }
-        const int64_t p0 = tp * 64, u0 = tu * 64;
-        const int np = (int)(g.cp - p0 < 64 ? g.cp - p0 : 64), nu = (int)(g.cu - u0 < 64 ? g.cu - u0 : 64);
+        const int64_t p0 = tp * XT_P, u0 = tu * XT_U;
+        const int np = (int)(g.cp - p0 < XT_P ? g.cp - p0 : XT_P), nu = (int)(g.cu - u0 < XT_U ? g.cu - u0 : XT_U);
         if (ALIGNED) {
-            if (np == 64 && nu == 64)
-                xpose_tile<Op, GATHER, true>(src, dst, g, pbase, ubase, p0, u0, np, nu, tile, fill, bad);
+            if (np == XT_P && nu == XT_U)
+                xpose_tile<Op, GATHER, true, TU, SC1>(src, dst, g, pbase, ubase, p0, u0, np, nu, tile, fill, bad);
             else
-                xpose_tile<Op, GATHER, false>(src, dst, g, pbase, ubase, p0, u0, np, nu, tile, fill, bad);
+                xpose_tile<Op, GATHER, false, TU, SC1>(src, dst, g, pbase, ubase, p0, u0, np, nu, tile, fill, bad);
         } else if (GATHER) {
             // user -> LDS, lanes along U
-            for (int r = hi2; r < np; r += 4)
-                if (lo6 < nu)
-                    tile[r][lo6] = ld_unaligned<TU>(src + (ubase + (p0 + r) * g.ip + (u0 + lo6) * g.iu) * UES);
+            for (int r = ru; r < np; r += RPP)
+                if (lu < nu)
+                    tile[r][lu] = ld_unaligned<TU>(src + (ubase + (p0 + r) * g.ip + (u0 + lu) * g.iu) * UES);
             __syncthreads();
             // LDS -> convert -> packed, lanes along P
-            for (int c = hi2; c < nu; c += 4)
-                if (lo6 < np) {
-                    uint8_t *pd = dst + (pbase + (u0 + c) * g.su + p0 + lo6) * PES;
+            for (int c = cp; c < nu; c += CPP)
+                if (lp < np) {
+                    uint8_t *pd = dst + (pbase + (u0 + c) * g.su + p0 + lp) * PES;
                     DU old = 0;
                     if constexpr (Op::PRESERVE) old = ld_unaligned<DU>(pd);
-                    st_unaligned<DU>(pd, Op::one(tile[lo6][c], old, fill, bad));
+                    st_unaligned<DU>(pd, Op::one(tile[lp][c], old, fill, bad));
                 }
         } else {
             // packed -> convert -> LDS, lanes along P
-            for (int c = hi2; c < nu; c += 4)
-                if (lo6 < np)
-                    tile[lo6][c] = Op::one(ld_unaligned<SU>(src + (pbase + (u0 + c) * g.su + p0 + lo6) * PES),
-                                           DU(0), fill, bad);
+            for (int c = cp; c < nu; c += CPP)
+                if (lp < np)
+                    tile[lp][c] = Op::one(ld_unaligned<SU>(src + (pbase + (u0 + c) * g.su + p0 + lp) * PES),
+                                          DU(0), fill, bad);
             __syncthreads();
             // LDS -> user, lanes along U
-            for (int r = hi2; r < np; r += 4)
-                if (lo6 < nu) st_unaligned<TU>(dst + (ubase + (p0 + r) * g.ip + (u0 + lo6) * g.iu) * UES, tile[r][lo6]);
+            for (int r = ru; r < np; r += RPP)
+                if (lu < nu) st_unaligned<TU>(dst + (ubase + (p0 + r) * g.ip + (u0 + lu) * g.iu) * UES, tile[r][lu]);
         }
         __syncthreads();
     }
@@ -821,8 +869,8 @@ inline bool transpose_geom(const pncxk_imap *m, TransposeGeom *g) {
     g->ip = m->imap[P];
     g->iu = m->imap[U];
     g->su = pst[U];
-    g->tp = (g->cp + 63) / 64;
-    g->tu = (g->cu + 63) / 64;
+    g->tp = (g->cp + XT_P - 1) / XT_P;
+    g->tu = (g->cu + XT_U - 1) / XT_U;
     g->nod = 0;
     int64_t outer = 1;
     for (int d = 0; d < P; d++) {

@@ -32,6 +32,8 @@ CASES = [
     ([65, 20, 130], [2, 130, 2600]),  # padded (imap 2) fastest user dim, outer dim between
     ([3, 40, 50], [2000, 1, 40]),     # U in the middle, outer dim first
     ([16, 16], [1, 16]),              # exactly one tile
+    ([200, 3, 130], [1, 200, 600]),   # 64 x 128 tiles: partial along U (72) and P (2)
+    ([256, 2, 128], [1, 256, 512]),   # whole 64 x 128 tiles only
 ]
 PAIRS = [(T.NC_INT, T.ITYPE_DOUBLE), (T.NC_SHORT, T.ITYPE_FLOAT), (T.NC_DOUBLE, T.ITYPE_DOUBLE),
          (T.NC_BYTE, T.ITYPE_INT), (T.NC_UINT64, T.ITYPE_SCHAR), (T.NC_FLOAT, T.ITYPE_FLOAT)]

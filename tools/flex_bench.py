@@ -1,6 +1,6 @@
 """Throughput of the fused pack+convert kernels (derived buftypes, varm) against
 the contiguous kernel on the same element count.  Device-resident; HIP events
-around each launch; algorithmic bytes = n * (xsize + isize) (the gaps between
+around 10 back-to-back launches; algorithmic bytes = n * (xsize + isize) (the gaps between
 runs are not counted).
 
 Workloads (NC_DOUBLE external <- double user buffer, put direction):
@@ -45,13 +45,17 @@ def main():
     def timeit(fn, n):
         fn()
         torch.cuda.synchronize()
+        # steady state: 10 launches of the same kernel between the events (a
+        # single launch after a different kernel moved results by ~10 points
+        # at these sizes, which are about the Infinity Cache's)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.reps)]
         for a, b in ev:
             a.record()
-            fn()
+            for _ in range(10):
+                fn()
             b.record()
         torch.cuda.synchronize()
-        ms = sorted(a.elapsed_time(b) for a, b in ev)[len(ev) // 2]
+        ms = sorted(a.elapsed_time(b) for a, b in ev)[len(ev) // 2] / 10
         return ms, n * 16 / ms / 1e6
 
     res = []

@@ -194,8 +194,11 @@ int main(int argc, char **argv) {
         pncx::TransposeGeom tg;
         if (!pncx::transpose_geom(&m, &tg)) { printf("no transpose geometry\n"); exit(1); }
         const unsigned grid = (unsigned)tg.ntiles;
-        add("product k_imap_tile (aligned)", [=] {
-            hipLaunchKernelGGL((pncx::k_imap_tile<pncx::SwapOp<8>, true, true>), dim3(grid), dim3(256), 0, 0,
+        add("product k_imap_tile sc1 stores", [=] {
+            hipLaunchKernelGGL((pncx::k_imap_tile<pncx::SwapOp<8>, true, true, true>), dim3(grid), dim3(256), 0, 0,
+                               (const uint8_t *)user, (uint8_t *)packed, tg, 0ULL, pncx::Sink{nullptr, nullptr, 0, 0}); });
+        add("product k_imap_tile (nt stores)", [=] {
+            hipLaunchKernelGGL((pncx::k_imap_tile<pncx::SwapOp<8>, true, true, false>), dim3(grid), dim3(256), 0, 0,
                                (const uint8_t *)user, (uint8_t *)packed, tg, 0ULL, pncx::Sink{nullptr, nullptr, 0, 0}); });
     }
     add("flat swap copy (same bytes)", [=] { hipLaunchKernelGGL(k_copy, dim3(n / 2 / 256), dim3(256), 0, 0,
