@@ -115,6 +115,28 @@ def test_no_cpu_fallback_without_gpu(built):
     assert rc == T.NC_EBADTYPE
 
 
+def test_ncmpii_in_swapn_aborts_without_gpu(built):
+    """ncmpii_in_swapn returns void upstream (common.h:151), so a device
+    failure cannot be reported: the shim aborts the process rather than
+    return with the buffer unswapped (pncx_ncmpii.c).  The child process
+    gets SIGABRT and says why."""
+    import subprocess
+    import sys
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible: the call would succeed")
+    lib = os.path.join(os.path.dirname(LIB), "libpncx_ncmpii.so")
+    code = ("import ctypes, numpy as np\n"
+            "L = ctypes.CDLL(%r)\n"
+            "b = np.arange(4, dtype=np.int64)\n"
+            "L.ncmpii_in_swapn(ctypes.c_void_p(b.ctypes.data), ctypes.c_longlong(4), 8)\n"
+            "print('returned')\n" % lib)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == -6, (r.returncode, r.stdout, r.stderr)
+    assert "returned" not in r.stdout
+    assert "ncmpii_in_swapn" in r.stderr
+
+
 def test_product_does_not_reference_oracle():
     """The product sources never include, link or load the oracle."""
     for d, _, files in os.walk(os.path.join(ROOT, "pnetcdf_amd")):
