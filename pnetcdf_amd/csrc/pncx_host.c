@@ -786,7 +786,10 @@ struct pncx_dtype {
     long long  np, nq;                /* pieces, 64-element chunks             */
     int        runmajor;              /* runs long enough for one wave each    */
     unsigned  *doff;                  /* device: byte offset - lo of each element
-                                       * of a copy (short-run tables, tmode 4) */
+                                       * of a copy (short-run tables, tmode 4), or
+                                       * (off16) one base per 64-element chunk
+                                       * followed by 16-bit offsets from it (tmode 5) */
+    int        off16;
 };
 
 /* Largest typemap (elements per copy) that gets a per-element offset map:
@@ -895,17 +898,48 @@ int pncx_type_commit(int itype, pncx_offset nblocks, const pncx_offset *disp,
         }
         free(h);
         if (!derr && !t->runmajor && t->tn <= toff_max_elems() && t->hi - t->lo <= 0xffffffffLL) {
-            /* short runs: per-element map (offsets from lo fit 32 bits) */
+            /* short runs: per-element map (offsets from lo fit 32 bits).
+             * When every 64-element chunk spans under 64 KiB the map is a
+             * 32-bit base per chunk plus 16-bit offsets: 2 B of HBM per
+             * element instead of 4 (PNCX_TOFF16=0 keeps 32 bits) */
             unsigned *o = (unsigned *)malloc(sizeof(unsigned) * (size_t)t->tn);
+            const char *e16 = getenv("PNCX_TOFF16");
+            size_t bytes = sizeof(unsigned) * (size_t)t->tn;
+            void *up = o;
             if (o == NULL) derr = NC_ENOMEM;
             for (i = 0; i < k && !derr; i++) {
                 const long long ln = (i + 1 < k ? t->pre[i + 1] : t->tn) - t->pre[i];
                 for (e = 0; e < ln; e++) o[t->pre[i] + e] = (unsigned)(t->disp[i] - t->lo + e * isz);
             }
-            if (!derr && (pncxrt_malloc((void **)&t->doff, sizeof(unsigned) * (size_t)t->tn) != 0 ||
-                          pncxrt_memcpy_h2d(t->doff, o, sizeof(unsigned) * (size_t)t->tn, NULL) != 0 ||
+            if (!derr && (e16 == NULL || atoi(e16) != 0)) {
+                const long long nq16 = (t->tn + 63) / 64;
+                unsigned *base = (unsigned *)malloc(sizeof(unsigned) * (size_t)nq16 + sizeof(unsigned short) * (size_t)t->tn);
+                int fits = base != NULL;
+                for (q = 0; q < nq16 && fits; q++) {
+                    const long long r1 = 64 * q + 64 < t->tn ? 64 * q + 64 : t->tn;
+                    unsigned mn = o[64 * q], mx = o[64 * q];
+                    for (e = 64 * q + 1; e < r1; e++) {
+                        if (o[e] < mn) mn = o[e];
+                        if (o[e] > mx) mx = o[e];
+                    }
+                    base[q] = mn;
+                    fits = mx - mn <= 0xffffu;
+                }
+                if (fits) {
+                    unsigned short *d16 = (unsigned short *)(base + nq16);
+                    for (e = 0; e < t->tn; e++) d16[e] = (unsigned short)(o[e] - base[e >> 6]);
+                    bytes = sizeof(unsigned) * (size_t)nq16 + sizeof(unsigned short) * (size_t)t->tn;
+                    up = base;
+                    t->off16 = 1;
+                } else {
+                    free(base);
+                }
+            }
+            if (!derr && (pncxrt_malloc((void **)&t->doff, bytes) != 0 ||
+                          pncxrt_memcpy_h2d(t->doff, up, bytes, NULL) != 0 ||
                           pncxrt_stream_sync(NULL) != 0))
                 derr = PNCX_EDEVICE;
+            if (up != o) free(up);
             free(o);
         }
         if (derr) {
@@ -987,8 +1021,10 @@ static int flex_layout(int ndims, const pncx_offset *count, const pncx_offset *i
         *lo = t->nblk ? t->disp0 : 0;
         return 0;
     }
-    m->tmode = t->layout == 2 && t->runmajor && packed_order ? 3 : t->layout == 2 && t->doff ? 4 : t->layout;
+    m->tmode = t->layout == 2 && t->runmajor && packed_order ? 3
+             : t->layout == 2 && t->doff ? (t->off16 ? 5 : 4) : t->layout;
     m->toff = t->doff;
+    m->toff16 = t->off16 ? (const unsigned short *)(t->doff + (t->tn + 63) / 64) : NULL;
     m->tlo = t->lo;
     m->tn = t->tn;
     m->textent = t->extent;

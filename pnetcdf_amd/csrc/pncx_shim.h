@@ -77,7 +77,8 @@ typedef struct pncxk_imap {
      *          tdisp[b] = its byte displacement (device arrays; tpre[tnblk] = tn)
      *       3: the same table, runs long enough for one wave per run (packed
      *          order only; runs split into pieces of <= PNCX_TMAP_PIECE)
-     *       4: the same table, short runs: per-element byte map toff */
+     *       4: the same table, short runs: per-element byte map toff
+     *       5: the same, 16-bit map: element r at tlo + toff[r >> 6] + toff16[r] */
     int       tmode;
     int       tpad;
     long long tn, textent, tlen, tstride, tdisp0, tnblk;
@@ -88,6 +89,9 @@ typedef struct pncxk_imap {
      * is at byte tlo + toff[r] (device array of tn, built at commit) */
     const unsigned  *toff;
     long long        tlo;
+    /* tmode 5: toff holds one base per 64-element chunk, toff16 the offsets
+     * from it (2 B per element instead of 4: chunks spanning < 64 KiB) */
+    const unsigned short *toff16;
 } pncxk_imap;
 
 typedef struct pncxk_opinfo {

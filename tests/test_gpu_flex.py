@@ -173,6 +173,28 @@ def test_flex_table_search_path(torch_cuda, where, monkeypatch):
 
 
 @pytest.mark.parametrize("where", ["host", "dev"])
+@pytest.mark.parametrize("map16", ["1", "0"])
+@pytest.mark.parametrize("gap", [5, 3000])
+def test_flex_offset_map_widths(torch_cuda, where, map16, gap, monkeypatch):
+    """short-run tables get a 16-bit offset map (a base per 64-element chunk,
+    tmode 5) when every chunk spans under 64 KiB, else the 32-bit map (tmode
+    4); PNCX_TOFF16=0 forces 32 bits.  Gaps of up to 3000 elements make
+    chunks span ~1.5 MiB of doubles (32-bit map by necessity); partial last
+    chunk and several copies included."""
+    monkeypatch.setenv("PNCX_TOFF16", map16)
+    rng = np.random.default_rng(gap + int(map16))
+    nb = 5000
+    blen = rng.integers(1, 8, nb)
+    gaps = rng.integers(0, gap, nb)
+    disp = np.concatenate([[0], np.cumsum(blen + gaps)[:-1]]).astype(np.int64)
+    dt = run_case(torch_cuda, where, T.NC_FLOAT, T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(),
+                  int(disp[-1] + blen[-1] + 5), 3, None, None, 21)
+    assert dt.inq()["layout"] == 2
+    # through a transposing imap as well (imap offset -> typemap stage)
+    run_case(torch_cuda, where, T.NC_INT, T.ITYPE_INT, [9, 0, 20, 3, 40], [2, 1, 5, 1, 3], 50, 4, [12, 4], [1, 12], 22)
+
+
+@pytest.mark.parametrize("where", ["host", "dev"])
 @pytest.mark.parametrize("imap", [False, True])
 def test_flex_long_runs(torch_cuda, where, imap):
     """runs of 50..1500 elements: one wave per run piece (k_tmap_runs, runs
