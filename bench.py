@@ -314,7 +314,7 @@ class C4Batch(Workload):
             self.launch = lambda: _ok(lib.pncx_dev_batch_async(arr, nvar, dstp, sptr))
         else:
             self.launch = lambda: _ok(lib.pncx_dev_batch(arr, nvar, stv, sptr), T.NC_ERANGE if self._erange else 0)
-            self.lib_timed = True
+        self.lib_timed = True        # kernel time: the library's dispatch-stamped events
         # algorithmic bytes: isz + xsz per element, summed over the variables
         per_pair = (4 + 2) + (4 + 4) if self._erange else (2 + 2) + (4 + 4)
         self.elems = nvar * nel

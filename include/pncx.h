@@ -321,12 +321,12 @@ int pncx_dev_batch_async(const pncx_seg *segs, int nseg, int *dstatus,
                          pncx_stream_t stream);
 
 /* Measurement aid (no reference counterpart): with timing enabled, every
- * pncx_dev_batch call on the current device records HIP events on its stream
- * around its batch kernels only (not the descriptor upload, the status copy
- * or the wait; pncx_dev_batch_async calls are not timed).
- * pncx_dev_batch_kernel_ms returns the summed kernel time and
- * the number of calls timed since pncx_dev_batch_timing(1) (which resets
- * both). */
+ * pncx_dev_batch and pncx_dev_batch_async call on the current device has
+ * its batch kernels stamped with HIP events by their own dispatches (start
+ * of the first class kernel, end of the last; not the descriptor upload,
+ * the status copy or the wait).  pncx_dev_batch_kernel_ms waits for the
+ * calls still queued and returns the summed kernel time and the number of
+ * calls timed since pncx_dev_batch_timing(1) (which resets both). */
 int pncx_dev_batch_timing(int enable);
 int pncx_dev_batch_kernel_ms(double *total_ms, long long *calls);
 

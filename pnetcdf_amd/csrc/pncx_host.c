@@ -1513,10 +1513,11 @@ static int dev_batch(const pncx_seg *segs, int nseg, int *status_out, int *dstat
         if (async && c->async_pending && c->async_stream != stream) err = pncxrt_stream_sync(c->async_stream);
         if (!err)
             err = launch_classes(c->cache_cls, c->cache_ncls, (uint8_t *)c->dscratch, c->cache_soff,
-                                 c->cache_moff, sval, 0, stream, async ? NULL : c);
+                                 c->cache_moff, sval, 0, stream, c);
         if (async && !err) {
             c->async_pending = 1;
             c->async_stream = stream;
+            if (c->timing) batch_time(c);       /* events read at the next drain */
         }
         if (!async) {
             /* byte swaps and copies never raise NC_ERANGE: no statuses to bring back */
@@ -1565,9 +1566,10 @@ static int dev_batch(const pncx_seg *segs, int nseg, int *status_out, int *dstat
         err = ensure_scratch(c, moff + sizeof(int) * (size_t)plan.map_ints + 16);
         if (!err)
             err = batch_run(&plan, nseg, (uint8_t *)c->dscratch, (uint8_t *)c->hscratch, soff, moff, sval, stream,
-                            async ? NULL : c, async ? dstatus : (int *)c->dscratch);
+                            c, async ? dstatus : (int *)c->dscratch);
         if (async) {
             if (!err) { c->async_pending = 1; c->async_stream = stream; }
+            if (!err && c->timing) batch_time(c);
         } else {
             /* the status words were zeroed by the upload; a batch of swaps
              * and copies only has nothing to read */

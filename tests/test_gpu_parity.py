@@ -418,6 +418,30 @@ def test_dev_batch_kernel_timing(torch_cuda):
     assert L.pncx_dev_batch_kernel_ms(ctypes.byref(tot), ctypes.byref(calls)) == 0 and calls.value == 0
     exp = np.arange(sizes[1], dtype=">f4").tobytes()
     assert outs[1].cpu().numpy().tobytes() == exp
+    # async calls are timed too; more calls than the event ring holds (256)
+    dst = torch.zeros(3, dtype=torch.int32, device="cuda")
+    assert L.pncx_dev_batch_timing(1) == 0
+    for _ in range(300):
+        assert L.pncx_dev_batch_async(arr, 3, ctypes.c_void_p(dst.data_ptr()), None) == 0
+    assert L.pncx_dev_batch_kernel_ms(ctypes.byref(tot), ctypes.byref(calls)) == 0
+    assert calls.value == 300 and 0 < tot.value < 10000
+    # two classes and a flag reduce (float -> NC_SHORT with NC_ERANGE + a swap):
+    # the stop event goes on the reduce
+    vals = torch.tensor([1.0, 4e4, -2.0, 7.0] * 4096, dtype=torch.float32, device="cuda")
+    xs = torch.zeros(vals.numel() * 2, dtype=torch.uint8, device="cuda")
+    fill = (ctypes.c_uint8 * 8)(0x01, 0x80)
+    arr2 = (pncx.Seg * 2)(pncx.Seg(T.PNCX_PUT, 5, T.NC_SHORT, T.ITYPE_FLOAT, vals.numel(), xs.data_ptr(),
+                                   vals.data_ptr(), ctypes.cast(fill, ctypes.c_void_p).value), arr[0])
+    st2 = (ctypes.c_int * 2)()
+    assert L.pncx_dev_batch_timing(1) == 0
+    for _ in range(4):
+        assert L.pncx_dev_batch(arr2, 2, st2, None) == T.NC_ERANGE
+        assert list(st2) == [T.NC_ERANGE, 0]
+    assert L.pncx_dev_batch_kernel_ms(ctypes.byref(tot), ctypes.byref(calls)) == 0
+    assert calls.value == 4 and 0 < tot.value < 1000
+    assert L.pncx_dev_batch_timing(0) == 0
+    got = xs.cpu().numpy()[:8].tobytes()
+    assert got == bytes([0x00, 0x01, 0x80, 0x01, 0xff, 0xfe, 0x00, 0x07])
 
 
 def test_dev_batch_async(torch_cuda):
