@@ -14,7 +14,8 @@
  * therefore go through mmap + memcpy: the pool first grows the file with
  * fallocate (never shrinks it, so ranks writing disjoint records of one file
  * stay safe), then each task maps its page-aligned window.  Runs under
- * MMAP_MIN bytes, file systems without fallocate and PNCX_IO_MMAP=0 use
+ * MMAP_MIN bytes (unless many of them fill a span densely: one mapping per
+ * share then), file systems without fallocate and PNCX_IO_MMAP=0 use
  * pwrite.  Reads use pread, which takes the shared lock and scales.
  */
 #define _GNU_SOURCE
@@ -38,7 +39,8 @@
 typedef struct task {
     struct task *next;
     pio_batch *b;
-    int fd, write;                   /* write: 1 = pwrite, 2 = mmap + memcpy for large runs */
+    int fd, write;                   /* write: 1 = pwrite, 2 = mmap + memcpy for large runs,
+                                      * 3 = one mapping per share over many small runs */
     pio_run *runs;                   /* shared by the tasks of one job */
     size_t n;
     long long lo, hi;                /* byte range of the concatenated runs */
@@ -91,12 +93,55 @@ static int map_write(int fd, const unsigned char *src, size_t n, long long off)
     return NC_NOERR;
 }
 
+/* Many small write runs (e.g. the rows of a rank's subarray): one mapping
+ * over the file span of this share, then a memcpy per run.  pwrite of 8 KiB
+ * rows took ~2 us each and serialised the ranks writing one file on the
+ * inode lock (the reference's benchmarks/C/pnetcdf_put_vara.c, 4 ranks:
+ * 1 GiB/s).  Returns 1 when the span is too sparse to map (caller pwrites). */
+static int span_write(int fd, const pio_run *runs, size_t n, long long lo, long long hi)
+{
+    long long pos = 0, fmin = -1, fmax = 0, bytes = hi - lo, base;
+    size_t i, span;
+    unsigned char *m;
+    for (i = 0; i < n && pos < hi; i++) {
+        const long long a = pos, b = pos + runs[i].len;
+        pos = b;
+        if (b <= lo) continue;
+        {
+            const long long s = a > lo ? a : lo, e = b < hi ? b : hi, k = s - a;
+            if (fmin < 0 || runs[i].off + k < fmin) fmin = runs[i].off + k;
+            if (runs[i].off + k + (e - s) > fmax) fmax = runs[i].off + k + (e - s);
+        }
+    }
+    if (fmin < 0) return 0;
+    if (fmax - fmin > 4 * bytes) return 1;
+    base = fmin - fmin % g_page;
+    span = (size_t)(fmax - base);
+    m = (unsigned char *)mmap(NULL, span, PROT_WRITE, MAP_SHARED, fd, (off_t)base);
+    if (m == MAP_FAILED) return 1;
+    for (i = 0, pos = 0; i < n && pos < hi; i++) {
+        const long long a = pos, b = pos + runs[i].len;
+        pos = b;
+        if (b <= lo) continue;
+        {
+            const long long s = a > lo ? a : lo, e = b < hi ? b : hi, k = s - a;
+            memcpy(m + (runs[i].off + k - base), runs[i].mem + k, (size_t)(e - s));
+        }
+    }
+    munmap(m, span);
+    return 0;
+}
+
 /* copy bytes [lo, hi) of the concatenation of runs */
 static int do_range(int fd, int write, const pio_run *runs, size_t n, long long lo, long long hi)
 {
     long long pos = 0;
     size_t i;
     int err = NC_NOERR;
+    if (write == 3) {
+        if (span_write(fd, runs, n, lo, hi) == 0) return NC_NOERR;
+        write = 1;
+    }
     for (i = 0; i < n && pos < hi && !err; i++) {
         const long long a = pos, b = pos + runs[i].len;
         pos = b;
@@ -127,22 +172,32 @@ static int mmap_mode(void)
     return v;
 }
 
-/* Write job through mappings?  The file must already cover every large run:
- * grow it with fallocate where needed (a mapping cannot extend a file). */
+/* Write job through mappings?  Large runs (>= MMAP_MIN) are each mapped;
+ * a job of small runs whose file span is at most 4x its bytes is mapped one
+ * span per share.  The file must already cover what is mapped: grow it with
+ * fallocate where needed (a mapping cannot extend a file). */
 static int write_mode(int fd, const pio_run *runs, size_t n, long long total)
 {
     struct stat st;
-    long long end = 0;
+    long long end = 0, fmin = -1, fmax = 0;
     size_t i;
+    int mode = 2;
     if (!mmap_mode() || total < (long long)MMAP_MIN) return 1;
-    for (i = 0; i < n; i++)
+    for (i = 0; i < n; i++) {
         if (runs[i].len >= (long long)MMAP_MIN && runs[i].off + runs[i].len > end) end = runs[i].off + runs[i].len;
-    if (end == 0) return 1;
+        if (runs[i].len > 0 && (fmin < 0 || runs[i].off < fmin)) fmin = runs[i].off;
+        if (runs[i].off + runs[i].len > fmax) fmax = runs[i].off + runs[i].len;
+    }
+    if (end == 0) {
+        if (fmin < 0 || fmax - fmin > 4 * total) return 1;
+        end = fmax;
+        mode = 3;
+    }
     if (fstat(fd, &st) != 0) return 1;
     if (end > (long long)st.st_size &&
         fallocate(fd, 0, (off_t)st.st_size, (off_t)(end - (long long)st.st_size)) != 0)
         return 1;
-    return 2;
+    return mode;
 }
 
 /* one share of a job is done: record its error, release the shared runs */
