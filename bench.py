@@ -95,6 +95,21 @@ def splitmix_uniform(torch, out, seed, lo, hi):
     del bits, u
 
 
+def host_cpu():
+    """The host CPU model and the logical CPUs visible (report
+    nproc and the model beside the CPU baselines)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"model": model, "nproc": os.cpu_count()}
+
+
 def cpu_baseline_swap8(budget_s=12.0, slab_bytes=2 << 30):
     """The oracle's ncmpii_in_swapn restatement (gcc -O2, 1 core) on a
     bounded host sample of the same workload."""
@@ -113,7 +128,8 @@ def cpu_baseline_swap8(budget_s=12.0, slab_bytes=2 << 30):
     moved = 16.0 * n * passes
     return {"value": round(moved / el / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"{slab_bytes >> 30} GiB NC_DOUBLE host slab, {passes} in-place 8-byte swap passes "
-                      f"in {el:.1f} s (oracle/pncx_oracle.c orc_in_swapn, gcc -O2, 1 thread)"}
+                      f"in {el:.1f} s (oracle/pncx_oracle.c orc_in_swapn, gcc -O2, 1 thread)",
+            "host": host_cpu()}
 
 
 def cpu_baseline_swap8_threads(budget_s=4.0, slab_bytes=2 << 30, threads=None):
