@@ -221,10 +221,12 @@ struct Sink {
     int  sval;     // the value a status word gets
 };
 
-__device__ __forceinline__ void publish(const Sink &s, int *status, bool bad) {
+// fidx: the block's flag slot -- its launch index, or for the batch kernels
+// the logical (XCD-remapped) block whose segment k_flags_batch looks up
+__device__ __forceinline__ void publish(const Sink &s, int *status, bool bad, int64_t fidx = -1) {
     if (s.flags != nullptr) {
         // every thread of the block reaches this (kernels publish at the end)
-        if (__syncthreads_or(bad) && threadIdx.x == 0) s.flags[blockIdx.x] = s.epoch;
+        if (__syncthreads_or(bad) && threadIdx.x == 0) s.flags[fidx < 0 ? (int64_t)blockIdx.x : fidx] = s.epoch;
     } else {
         publish_status(status, bad, s.sval);
     }
@@ -279,6 +281,15 @@ __device__ __forceinline__ int batch_segment(long long b, long long uniform, con
 __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nb) {
     const int64_t q = nb >> 3, r = nb & 7, x = b & 7;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
+// the batch kernels' logical block (segment lookup, flag slot): XCD-contiguous
+// unless built with -DPNCX_BATCH_REMAP=0 (the A/B probe tools/c4_ab.py)
+#ifndef PNCX_BATCH_REMAP
+#define PNCX_BATCH_REMAP 1
+#endif
+__device__ __forceinline__ int64_t batch_block() {
+    return PNCX_BATCH_REMAP ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
 }
 
 // One vector step per lane ("one-shot" grid): measured 6.6 TB/s for the
@@ -474,7 +485,7 @@ __global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg, 
                                                const int *map, pncxk_groups grp, Sink sk) {
     using S = Shape<Op>;
     __shared__ __attribute__((aligned(16))) uint8_t lds[S::USE_LDS ? 4096 : 16];
-    const long long b = blockIdx.x;
+    const long long b = batch_block();   // logical block: segment lookup and flag slot
     const int lo = batch_segment(b, uniform, map, grp, segs, nseg);
     const pncxk_seg sg = segs[lo];
     const uint8_t *src = (const uint8_t *)sg.src;
@@ -490,7 +501,7 @@ __global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg, 
     if (rel < ntile)
         tile_body<Op, NT>(src + (sg.head + rel * (int64_t)S::TILE) * S::SS,
                           dst + (sg.head + rel * (int64_t)S::TILE) * S::DS, fill, bad, lds);
-    publish(sk, sg.status, bad);
+    publish(sk, sg.status, bad, b);
 }
 
 // ---------------------------------------------------------------------------

@@ -297,18 +297,15 @@ constexpr int MIX_LANES = PNCXK_MIX_LANES;
 
 // One launch for all same-type segments of a batch (C4: NC_SHORT and
 // NC_FLOAT iputs): the block's segment says its element size.  A block is
-// MIX_LANES lanes x 16 B (one nontemporal vector each, no loop).  On the C4
-// shape (1.5 GiB moved over 512 buffers) block size and order change the rate
-// by less than the spread between processes: 256/512/1024 lanes all land at
-// 77-87 % of HBM peak depending on where the buffers were placed, against
-// 81-83 % for one contiguous buffer of the same bytes (tools/batch_sweep.hip,
-// profiles/r01_batch_sweep*.txt).  1024 lanes = 4x fewer blocks to schedule.
-// Round 2, in this kernel and one process (tools/c4_placement.py,
-// profiles/r02_c4_placement*.jsonl): one allocation per buffer, torch
-// sub-allocations, one pool and two flat segments all run at 77-79 % of
-// peak, so placement does not explain the gap; plain (write-back) stores
-// lose 1-4 points to "nt sc1" on every placement.  Persistent grids that
-// prefetch their next tile ran at 65-74 % (tools/c4_store_sweep.hip).
+// MIX_LANES lanes x 16 B (one nontemporal vector each, no loop), blocks in
+// XCD-contiguous order.  Round 2 (tools/c4_shape_sweep.hip, 256 buffer pairs,
+// splitmix64 data, three boxes): launch order at 1024 lanes 75.8-77.1 % of
+// peak, XCD-contiguous order 80.3-82.7 % at 256, 512 or 1024 lanes; the same
+// descriptors pointing into one allocation per side 83.3-84.1 %, one flat
+// buffer pair 83.4-84.5 %.  Two or four vectors per lane lose 1-5 points.
+// Plain (write-back) stores lose 1-4 points to "nt sc1" in the library
+// (tools/c4_placement.py); persistent grids that prefetch their next tile
+// ran at 65-74 % (tools/c4_store_sweep.hip).
 __device__ __forceinline__ u32x4 swap16(u32x4 v, int es) {
     u32x4 r = v;
     if (es == 2) {
@@ -333,7 +330,10 @@ __device__ __forceinline__ void mix_scalar(const uint8_t *src, uint8_t *dst, int
 
 __global__ __launch_bounds__(MIX_LANES) void k_batch_swapmix(const pncxk_seg *segs, int nseg, long long uniform,
                                                              const int *map, pncxk_groups grp) {
-    const long long b = blockIdx.x;
+    // XCD-contiguous block order (each XCD takes one contiguous run of
+    // tiles): 75.8-77.1 % -> 80.3-82.7 % of peak on the C4 layout at 1024
+    // lanes, three boxes (tools/c4_shape_sweep.hip, profiles/r02_c4_shape_sweep*.txt)
+    const long long b = batch_block();
     const int s = batch_segment(b, uniform, map, grp, segs, nseg);
     const pncxk_seg sg = segs[s];
     const uint8_t *src = (const uint8_t *)sg.src;
