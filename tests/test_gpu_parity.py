@@ -717,3 +717,102 @@ def test_large_conversions_every_element(torch_cuda):
         pncx.dev_getn(5, T.NC_FLOAT, be(f), of, n, T.ITYPE_FLOAT, st)
         torch.cuda.synchronize()
         assert torch.equal(of, f), rep
+
+
+def _fuzz_segments(torch, rng, ora, nseg):
+    """Random segments over every (cdf, xtype, itype) pair and both directions:
+    sizes 0..40000 (a few large), byte offsets 0..15 on both buffers, put
+    fills that are the default, a user value or NULL (the existing external
+    bytes are kept where the codec reads them); expected bytes from the oracle."""
+    def dev(nbytes, off, data=b""):
+        t = torch.zeros(off + nbytes + 16, dtype=torch.uint8, device="cuda")
+        if data:
+            t[off:off + len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+        return t
+
+    segs, refs = [], []
+    for _ in range(nseg):
+        cdf, xt, it, _k = PAIRS[int(rng.integers(0, len(PAIRS)))]
+        d = T.PNCX_GET if rng.random() < 0.5 else T.PNCX_PUT
+        n = int(rng.integers(0, 40000)) if rng.random() < 0.9 else int(rng.integers(200000, 600000))
+        ox, oi = int(rng.integers(0, 16)), int(rng.integers(0, 16))
+        xs, isz = T.xlen(xt), T.ilen(it)
+        if rng.random() < 0.5:
+            raw = rng.integers(0, 256, n * 8, dtype=np.uint8).tobytes()       # any bits
+        else:                                                                 # small values: mostly in range
+            raw = rng.integers(-100, 100, n).astype(np.int64).tobytes()
+        fill = None
+        if d == T.PNCX_GET:
+            xin = raw[: n * xs]
+            exp, so = ora.getn(cdf, xt, xin, it)
+            dx, di = dev(n * xs, ox, xin), dev(n * isz, oi)
+            refs.append((di, oi, exp.tobytes(), so, n * isz, None))
+        else:
+            if T.ITYPE_NP[it] in (np.float32, np.float64) and rng.random() < 0.5:
+                ib = rng.uniform(-1e5, 1e5, n).astype(T.ITYPE_NP[it])
+            else:
+                ib = np.frombuffer(raw[: n * isz], T.ITYPE_NP[it]).copy()
+            u = rng.random()
+            if u < 0.4:
+                fill = T.fill_bytes(xt)
+            elif u < 0.8:
+                fill = rng.integers(0, 256, xs, dtype=np.uint8).tobytes()
+            xinit = rng.integers(0, 256, n * xs, dtype=np.uint8).tobytes()
+            xb, so = ora.putn(cdf, xt, ib, it, fill, xinit=xinit if fill is None else None)
+            dx, di = dev(n * xs, ox, xinit), dev(n * isz, oi, ib.tobytes())
+            refs.append((dx, ox, xb, so, n * xs, xinit if fill is None else None))
+        segs.append(dict(dir=d, cdf_ver=cdf, xtype=xt, itype=it, nelems=n, xbuf=dx[ox:], ibuf=di[oi:], fill=fill))
+    return segs, refs
+
+
+def _check_refs(refs, st):
+    for k, ((buf, off, exp, so, nb, _x), stv) in enumerate(zip(refs, st)):
+        assert stv == so, (k, stv, so)
+        got = buf[off:off + nb].cpu().numpy().tobytes()
+        assert got == exp, k
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def _reset_outputs(torch, refs):
+    """zero the outputs, or restore the prior external bytes a NULL fill keeps"""
+    for buf, off, exp, so, nb, xinit in refs:
+        buf[off:off + nb] = 0
+        if xinit:
+            buf[off:off + nb] = torch.frombuffer(bytearray(xinit), dtype=torch.uint8).cuda()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_dev_batch_fuzz_all_pairs(torch_cuda, seed):
+    """Random batches over all 221 pairs x both directions (misaligned, NULL /
+    default / user fills), synchronous and asynchronous, each called twice
+    (the second call reuses the cached plan, after the outputs are reset):
+    bit-exact outputs and statuses against the oracle every time."""
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    ora = OracleConv()
+    rng = np.random.default_rng(0xF022 + seed)
+    segs, refs = _fuzz_segments(torch, rng, ora, 90)
+    _check_refs(refs, pncx.dev_batch(segs))
+    _reset_outputs(torch, refs)
+    _check_refs(refs, pncx.dev_batch(segs))
+    # asynchronous form on fresh inputs: statuses land in device words
+    segs, refs = _fuzz_segments(torch, rng, ora, 90)
+    arr = (pncx.Seg * len(segs))()
+    keep = []
+    for k, s in enumerate(segs):
+        fb = None
+        if s["fill"] is not None:
+            fb = np.frombuffer(bytes(s["fill"]) + b"\0" * 8, np.uint8).copy()
+            keep.append(fb)
+        arr[k] = pncx.Seg(s["dir"], s["cdf_ver"], s["xtype"], s["itype"], s["nelems"], s["xbuf"].data_ptr(),
+                          s["ibuf"].data_ptr(), None if fb is None else fb.ctypes.data)
+    dst = torch.zeros(len(segs), dtype=torch.int32, device="cuda")
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for rep in range(2):
+        if rep:
+            _reset_outputs(torch, refs)
+            dst.zero_()
+        rc = pncx.lib().pncx_dev_batch_async(arr, len(segs), ctypes.c_void_p(dst.data_ptr()), sp)
+        assert rc in (T.NC_NOERR, T.NC_ERANGE), rc
+        torch.cuda.synchronize()
+        _check_refs(refs, dst.cpu().tolist())
