@@ -305,6 +305,8 @@ typedef struct ctx_t {
     int    timing;            /* pncx_dev_batch_timing: events around the batch kernels */
     void  *tev[2 * NTEV];     /* start/stop event pairs of the timed calls not yet read */
     int    tpend;             /* pairs in use */
+    int    tcpend;            /* timed calls whose pairs are not read yet */
+    int    tnext;             /* pairs the call being launched uses      */
     double tms;               /* summed kernel time of the timed batch calls */
     long long tcalls;         /* ... and their number                         */
     unsigned long long *dfirst;   /* pncx_dev_first_diff result word */
@@ -1360,18 +1362,19 @@ static void batch_time_drain(ctx_t *c)
     for (k = 0; k < c->tpend; k++) {
         float ms = 0.0f;
         if (pncxrt_event_sync(c->tev[2 * k + 1]) == 0 &&
-            pncxrt_event_elapsed_ms(&ms, c->tev[2 * k], c->tev[2 * k + 1]) == 0) {
+            pncxrt_event_elapsed_ms(&ms, c->tev[2 * k], c->tev[2 * k + 1]) == 0)
             c->tms += ms;
-            c->tcalls++;
-        }
     }
-    c->tpend = 0;
+    c->tcalls += c->tcpend;
+    c->tpend = c->tcpend = 0;
 }
 
-/* the call that used pair tpend has completed */
+/* the call whose launches used the c->tnext pairs after tpend has completed */
 static void batch_time(ctx_t *c)
 {
-    if (++c->tpend == NTEV) batch_time_drain(c);
+    c->tpend += c->tnext;
+    c->tnext = 0;
+    c->tcpend++;
 }
 
 /* launch the class kernels of a plan whose descriptors are on the device */
@@ -1379,12 +1382,17 @@ static int launch_classes(const cls_t *cls, int ncls, uint8_t *dbase, size_t sof
                           int build_maps, void *stream, ctx_t *tc)
 {
     int k, err = 0;
-    /* timing: the start event is stamped by the first class kernel's own
-     * dispatch (hipExtLaunchKernel), not recorded ahead of it -- on an idle
-     * stream a recorded event would also time the host's launch call */
-    const int timed = tc != NULL && tc->timing;
-    void *ev0 = timed ? tc->tev[2 * tc->tpend] : NULL, *ev1 = timed ? tc->tev[2 * tc->tpend + 1] : NULL;
-    if (timed && ncls == 0) err = pncxrt_event_record(ev0, stream);
+    /* timing: every class kernel's start and end are stamped by its own
+     * dispatch (hipExtLaunchKernel), and a call's kernel time is the sum of
+     * those intervals, as rocprof's per-kernel durations add up.  Events
+     * recorded ahead of a kernel on an idle stream would also time the host's
+     * launch call, and a stamped kernel delays the next one on its stream by
+     * ~5 us, so an interval from the first kernel's start to the last one's
+     * end would count that gap too.  The flag reduce (k_flags_*) is not
+     * timed.  A call with more classes than the event ring holds goes untimed. */
+    const int timed = tc != NULL && tc->timing && ncls <= NTEV;
+    if (timed && tc->tpend + ncls > NTEV) batch_time_drain(tc);
+    if (tc != NULL) tc->tnext = 0;
     pncxk_seg *dseg = (pncxk_seg *)(dbase + soff);
     int *dmap = (int *)(dbase + moff);
     for (k = 0; k < ncls && !err; k++) {
@@ -1400,11 +1408,13 @@ static int launch_classes(const cls_t *cls, int ncls, uint8_t *dbase, size_t sof
         ba.stream = stream;
         ba.ev_start = ba.ev_stop = NULL;
         if (ba.dmap != NULL && build_maps) err = pncxk_batch_map(&ba);
-        if (timed && k == 0) ba.ev_start = ev0;
-        if (timed && k == ncls - 1) ba.ev_stop = ev1;
+        if (timed) {
+            ba.ev_start = tc->tev[2 * (tc->tpend + k)];
+            ba.ev_stop = tc->tev[2 * (tc->tpend + k) + 1];
+        }
         if (!err) err = pncxk_batch(c->op.kind, c->op.a, c->op.b, c->op.c, &ba);
+        if (!err && timed) tc->tnext = k + 1;
     }
-    if (!err && timed && ncls == 0) err = pncxrt_event_record(ev1, stream);
     return err;
 }
 
@@ -1641,7 +1651,7 @@ int pncx_dev_batch_timing(int enable)
             }
     }
     c->timing = enable != 0;
-    c->tpend = 0;
+    c->tpend = c->tcpend = c->tnext = 0;
     c->tms = 0.0;
     c->tcalls = 0;
     pthread_mutex_unlock(&c->lock);

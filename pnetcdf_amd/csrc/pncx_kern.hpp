@@ -235,8 +235,7 @@ __device__ __forceinline__ void publish(const Sink &s, int *status, bool bad, in
 // the launcher side (pncx_kern_swap.hip)
 Sink sink_acquire(int *status, int sval, hipStream_t st, int64_t nblocks, bool want);
 int sink_finish(const Sink &s, hipStream_t st, int64_t nblocks, int err);
-int sink_finish_batch(const Sink &s, const pncxk_seg *dsegs, int nseg, int64_t nblocks, hipStream_t st, int err,
-                      hipEvent_t ev_stop = nullptr);
+int sink_finish_batch(const Sink &s, const pncxk_seg *dsegs, int nseg, int64_t nblocks, hipStream_t st, int err);
 
 // can a conversion from S to D report NC_ERANGE at all (get1/put1 rules):
 // into a floating type only double -> float is checked; from a floating type
@@ -1009,16 +1008,16 @@ int launch_batch(const pncxk_batch_args *a) {
     if constexpr (Op::PRESERVE) return NC_EINVAL;   // host runs these one by one
     hipStream_t st = (hipStream_t)a->stream;
     const Sink sk = sink_acquire(nullptr, a->sval, st, a->nblocks, may_range<Op>::value);
-    // timing: the stop event goes on the flag reduce when there is one
+    // timing: both events are stamped by this kernel's dispatch (the flag
+    // reduce is not timed)
     hipEvent_t e0 = (hipEvent_t)a->ev_start, e1 = (hipEvent_t)a->ev_stop;
     if (e0 != nullptr || e1 != nullptr)
-        hipExtLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0, st, e0,
-                              sk.flags != nullptr ? nullptr : e1, 0, a->dsegs, a->nseg, a->uniform, a->dmap, a->grp, sk);
+        hipExtLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0, st, e0, e1, 0, a->dsegs,
+                              a->nseg, a->uniform, a->dmap, a->grp, sk);
     else
         hipLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0, st, a->dsegs, a->nseg,
                            a->uniform, a->dmap, a->grp, sk);
-    return sink_finish_batch(sk, a->dsegs, a->nseg, a->nblocks, st, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE,
-                             sk.flags != nullptr ? e1 : nullptr);
+    return sink_finish_batch(sk, a->dsegs, a->nseg, a->nblocks, st, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
 }
 
 template <class Op>

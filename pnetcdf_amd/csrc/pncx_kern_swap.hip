@@ -139,6 +139,11 @@ extern "C" int pncxk_fill(void *dst, long long nelems, int xsize, const void *xv
 // later call overwrite an earlier call's flags before its reduce reads them).
 // The mutex is held from sink_acquire to sink_finish so that one call's
 // kernel and reduce are enqueued back to back.
+// No event marks a reduce's completion: an event recorded after every reduce
+// delayed the next kernel on the stream by 5.8 us (the synchronous batch's
+// completion kernel, profiles/r02s_c4_erange trace).  A slot handed to
+// another stream or device, or regrown, is first drained with a device (or
+// stream) synchronize instead -- rare: it takes more than NFLAGSLOT streams.
 // ---------------------------------------------------------------------------
 namespace {
 struct FlagSlot {
@@ -147,7 +152,6 @@ struct FlagSlot {
     int *flags;
     int64_t cap;          // ints
     int epoch;
-    hipEvent_t done;      // recorded after the last reduce that read this array
     uint64_t tick;
     bool live;
 };
@@ -155,6 +159,14 @@ constexpr int NFLAGSLOT = 32;
 FlagSlot g_fslot[NFLAGSLOT];
 std::mutex g_fslot_mu;
 uint64_t g_ftick;
+
+// every kernel queued on the slot's device has finished (its stream may be
+// gone, so the whole device is drained)
+void drain_device(int dev, int cur) {
+    if (dev != cur) (void)hipSetDevice(dev);
+    (void)hipDeviceSynchronize();
+    if (dev != cur) (void)hipSetDevice(cur);
+}
 }  // namespace
 
 namespace pncx {
@@ -174,28 +186,24 @@ Sink sink_acquire(int *status, int sval, hipStream_t st, int64_t nblocks, bool w
     if (f == nullptr) {                 // take a free slot, or the least recently used one
         f = lru;
         if (f->live) {
-            (void)hipEventSynchronize(f->done);       // its last reduce has read the flags
+            drain_device(f->dev, dev);          // its last reduce has read the flags
             if (f->dev != dev) {
+                (void)hipSetDevice(f->dev);
                 (void)hipFree(f->flags);
-                (void)hipEventDestroy(f->done);
+                (void)hipSetDevice(dev);
                 f->flags = nullptr;
                 f->cap = 0;
-                f->done = nullptr;
             }
         }
         f->live = true;
         f->dev = dev;
         f->stream = st;     /* the epoch counter continues: the array may hold old epochs */
-        if (f->done == nullptr && hipEventCreateWithFlags(&f->done, hipEventDisableTiming) != hipSuccess) {
-            f->done = nullptr;
-            f->live = false;
-            g_fslot_mu.unlock();
-            return s;
-        }
     }
     if (f->cap < nblocks) {             // grow: wait for the array's last use on this stream
-        (void)hipEventSynchronize(f->done);
-        if (f->flags) (void)hipFree(f->flags);
+        if (f->flags) {
+            (void)hipStreamSynchronize(st);
+            (void)hipFree(f->flags);
+        }
         f->cap = nblocks > 2 * f->cap ? nblocks : 2 * f->cap;
         if (hipMalloc(&f->flags, sizeof(int) * (size_t)f->cap) != hipSuccess ||
             hipMemsetAsync(f->flags, 0, sizeof(int) * (size_t)f->cap, st) != hipSuccess) {
@@ -219,14 +227,7 @@ Sink sink_acquire(int *status, int sval, hipStream_t st, int64_t nblocks, bool w
     return s;                           // the mutex stays held until sink_finish*
 }
 
-static void sink_release(hipStream_t st) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    for (int i = 0; i < NFLAGSLOT; i++)
-        if (g_fslot[i].live && g_fslot[i].dev == dev && g_fslot[i].stream == st) {
-            (void)hipEventRecord(g_fslot[i].done, st);
-            break;
-        }
+static void sink_release(hipStream_t) {
     g_fslot_mu.unlock();
 }
 
@@ -270,16 +271,11 @@ int sink_finish(const Sink &s, hipStream_t st, int64_t nblocks, int err) {
     return err;
 }
 
-int sink_finish_batch(const Sink &s, const pncxk_seg *dsegs, int nseg, int64_t nblocks, hipStream_t st, int err,
-                      hipEvent_t ev_stop) {
+int sink_finish_batch(const Sink &s, const pncxk_seg *dsegs, int nseg, int64_t nblocks, hipStream_t st, int err) {
     if (s.flags == nullptr) return err;
     if (!err && nseg > 0) {
-        if (ev_stop != nullptr)
-            hipExtLaunchKernelGGL(k_flags_batch, dim3((unsigned)nseg), dim3(256), 0, st, nullptr, ev_stop, 0, dsegs,
-                                  nseg, nblocks, (const int *)s.flags, s.epoch, s.sval);
-        else
-            hipLaunchKernelGGL(k_flags_batch, dim3((unsigned)nseg), dim3(256), 0, st, dsegs, nseg, nblocks, s.flags,
-                               s.epoch, s.sval);
+        hipLaunchKernelGGL(k_flags_batch, dim3((unsigned)nseg), dim3(256), 0, st, dsegs, nseg, nblocks, s.flags,
+                           s.epoch, s.sval);
         if (hipGetLastError() != hipSuccess) err = PNCX_EDEVICE;
     }
     sink_release(st);

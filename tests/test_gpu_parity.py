@@ -426,7 +426,7 @@ def test_dev_batch_kernel_timing(torch_cuda):
     assert L.pncx_dev_batch_kernel_ms(ctypes.byref(tot), ctypes.byref(calls)) == 0
     assert calls.value == 300 and 0 < tot.value < 10000
     # two classes and a flag reduce (float -> NC_SHORT with NC_ERANGE + a swap):
-    # the stop event goes on the reduce
+    # each class kernel carries its own event pair, the reduce is not timed
     vals = torch.tensor([1.0, 4e4, -2.0, 7.0] * 4096, dtype=torch.float32, device="cuda")
     xs = torch.zeros(vals.numel() * 2, dtype=torch.uint8, device="cuda")
     fill = (ctypes.c_uint8 * 8)(0x01, 0x80)
