@@ -1224,6 +1224,17 @@ static int cmp_seg_size(const void *pa, const void *pb)
     return a->block0 < b->block0 ? -1 : a->block0 > b->block0;   /* keep plan order */
 }
 
+/* run k of a group table divides by per[k] with a multiply and a shift
+ * (pncx_shim.h): shr = 31 + ceil(log2 per), mag = ceil(2^shr / per) */
+static void group_magic(pncxk_groups *g, int k)
+{
+    const long long d = g->per[k];
+    int l = 0;
+    while ((1LL << l) < d) l++;
+    g->shr[k] = 31 + l;
+    g->mag[k] = ((1ULL << g->shr[k]) - 1) / (unsigned long long)d + 1;
+}
+
 /* Non-uniform class: sort its segments by block count and describe the runs
  * of equal counts (at most PNCXK_MAXGRP) -- O(1) block->segment in the
  * kernel without a map kernel.  Returns 0 when there are too many sizes. */
@@ -1245,6 +1256,7 @@ static int make_groups(pncxk_seg *seg, int count, pncxk_groups *g)
         b0 += nb;
     }
     g->n = n;
+    for (k = 0; k < n; k++) group_magic(g, k);
     return 1;
 }
 
@@ -1326,7 +1338,10 @@ static int batch_plan(plan_t *p)
         c->count = p->nsegd - c->first;
         memset(&c->grp, 0, sizeof c->grp);
         if (c->count > 0) {
-            if (c->uniform > 0) {
+            if (c->uniform > 0) {                  /* all equal: one run */
+                c->grp.n = 1;
+                c->grp.per[0] = c->uniform;
+                group_magic(&c->grp, 0);
                 c->map_off = -1;
             } else if (make_groups(p->seg + c->first, c->count, &c->grp)) {
                 c->uniform = 0;                    /* a few sizes: group table */
@@ -1401,7 +1416,6 @@ static int launch_classes(const cls_t *cls, int ncls, uint8_t *dbase, size_t sof
         ba.dsegs = dseg + c->first;
         ba.nseg = c->count;
         ba.nblocks = c->nblocks;
-        ba.uniform = c->uniform;
         ba.dmap = c->map_off >= 0 ? dmap + c->map_off : NULL;
         ba.grp = c->grp;
         ba.sval = sval;

@@ -253,16 +253,23 @@ template <int XT, int IT, bool P> struct may_range<PutOp<XT, IT, P>> {
     static constexpr bool value = range_loss<I<IT>, X<XT>>();
 };
 
-// block -> segment of a batch grid: equal-size segments divide directly, a
-// few runs of equal sizes (e.g. NC_SHORT and NC_FLOAT variables) scan the
-// group table passed by value, anything else reads the device map
-__device__ __forceinline__ int batch_segment(long long b, long long uniform, const int *map,
-                                             const pncxk_groups &g, const pncxk_seg *segs, int nseg) {
-    if (uniform > 0) return (int)(b / uniform);
+// block -> segment of a batch grid: a few runs of equal sizes (e.g. NC_SHORT
+// and NC_FLOAT variables; all-equal is one run) pick their run with
+// independent kernarg loads and divide by a host-computed multiply + shift;
+// anything else reads the device map.  Round 2 had a dependent load per run
+// and a 64-bit division here: 5.6 % slower than the same kernel with a
+// constant divisor on the C4 layout (tools/c4_placement.py --steady against
+// tools/c4_shape_sweep.hip, one box).
+__device__ __forceinline__ int batch_segment(long long b, const int *map, const pncxk_groups &g,
+                                             const pncxk_seg *segs, int nseg) {
     if (g.n > 0) {
-        int k = 0;
-        while (k + 1 < g.n && b >= g.b0[k + 1]) k++;
-        return g.s0[k] + (int)((b - g.b0[k]) / g.per[k]);
+        long long b0 = g.b0[0];
+        unsigned long long mag = g.mag[0];
+        int shr = g.shr[0], s0 = g.s0[0];
+#pragma unroll
+        for (int k = 1; k < PNCXK_MAXGRP; k++)
+            if (k < g.n && b >= g.b0[k]) { b0 = g.b0[k]; mag = g.mag[k]; shr = g.shr[k]; s0 = g.s0[k]; }
+        return s0 + (int)(((unsigned long long)(b - b0) * mag) >> shr);
     }
     if (map != nullptr) return map[b];
     int lo = 0, hi = nseg - 1;             // binary search (sorted by block0)
@@ -480,12 +487,12 @@ __global__ __launch_bounds__(256) void k_scalar(const uint8_t *src, uint8_t *dst
 constexpr int BATCH_STEPS = 1;  // tiles per block
 
 template <class Op, bool NT>
-__global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg, long long uniform,
-                                               const int *map, pncxk_groups grp, Sink sk) {
+__global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg, const int *map,
+                                               pncxk_groups grp, Sink sk) {
     using S = Shape<Op>;
     __shared__ __attribute__((aligned(16))) uint8_t lds[S::USE_LDS ? 4096 : 16];
     const long long b = batch_block();   // logical block: segment lookup and flag slot
-    const int lo = batch_segment(b, uniform, map, grp, segs, nseg);
+    const int lo = batch_segment(b, map, grp, segs, nseg);
     const pncxk_seg sg = segs[lo];
     const uint8_t *src = (const uint8_t *)sg.src;
     uint8_t *dst = (uint8_t *)sg.dst;
@@ -1013,10 +1020,10 @@ int launch_batch(const pncxk_batch_args *a) {
     hipEvent_t e0 = (hipEvent_t)a->ev_start, e1 = (hipEvent_t)a->ev_stop;
     if (e0 != nullptr || e1 != nullptr)
         hipExtLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0, st, e0, e1, 0, a->dsegs,
-                              a->nseg, a->uniform, a->dmap, a->grp, sk);
+                              a->nseg, a->dmap, a->grp, sk);
     else
         hipLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0, st, a->dsegs, a->nseg,
-                           a->uniform, a->dmap, a->grp, sk);
+                           a->dmap, a->grp, sk);
     return sink_finish_batch(sk, a->dsegs, a->nseg, a->nblocks, st, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
 }
 

@@ -324,13 +324,13 @@ __device__ __forceinline__ void mix_scalar(const uint8_t *src, uint8_t *dst, int
     for (int64_t e = e0 + threadIdx.x; e < e1; e += MIX_LANES) scalar_elem<Op>(src, dst, e, 0, bad);
 }
 
-__global__ __launch_bounds__(MIX_LANES) void k_batch_swapmix(const pncxk_seg *segs, int nseg, long long uniform,
-                                                             const int *map, pncxk_groups grp) {
+__global__ __launch_bounds__(MIX_LANES) void k_batch_swapmix(const pncxk_seg *segs, int nseg, const int *map,
+                                                             pncxk_groups grp) {
     // XCD-contiguous block order (each XCD takes one contiguous run of
     // tiles): 75.8-77.1 % -> 80.3-82.7 % of peak on the C4 layout at 1024
     // lanes, three boxes (tools/c4_shape_sweep.hip, profiles/r02_c4_shape_sweep*.txt)
     const long long b = batch_block();
-    const int s = batch_segment(b, uniform, map, grp, segs, nseg);
+    const int s = batch_segment(b, map, grp, segs, nseg);
     const pncxk_seg sg = segs[s];
     const uint8_t *src = (const uint8_t *)sg.src;
     uint8_t *dst = (uint8_t *)sg.dst;
@@ -360,11 +360,10 @@ extern "C" int pncxk_batch(int kind, int a, int b, int c, const pncxk_batch_args
         if (args->ev_start != nullptr || args->ev_stop != nullptr)
             hipExtLaunchKernelGGL(k, dim3((unsigned)args->nblocks), dim3(MIX_LANES), 0,
                                   (hipStream_t)args->stream, (hipEvent_t)args->ev_start, (hipEvent_t)args->ev_stop, 0,
-                                  args->dsegs, args->nseg, args->uniform, args->dmap, args->grp);
+                                  args->dsegs, args->nseg, args->dmap, args->grp);
         else
             hipLaunchKernelGGL(k, dim3((unsigned)args->nblocks), dim3(MIX_LANES), 0,
-                               (hipStream_t)args->stream, args->dsegs, args->nseg, args->uniform, args->dmap,
-                               args->grp);
+                               (hipStream_t)args->stream, args->dsegs, args->nseg, args->dmap, args->grp);
         return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
     }
     if (kind == PNCXK_SWAP) {

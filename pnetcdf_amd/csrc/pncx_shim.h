@@ -37,22 +37,26 @@ typedef struct pncxk_seg {
 } pncxk_seg;
 
 /* up to PNCXK_MAXGRP runs of equal-size segments: block b of the grid is in
- * group g when b0[g] <= b < b0[g+1], segment s0[g] + (b - b0[g]) / per[g] */
+ * group g when b0[g] <= b < b0[g+1], segment s0[g] + (b - b0[g]) / per[g].
+ * The division is a multiply and a shift: q = (r * mag[g]) >> shr[g] with
+ * mag = ceil(2^shr / per), shr = 31 + ceil(log2 per), exact for r < 2^31
+ * (a class grid never reaches 2^31 blocks: that would be >= 8 TiB). */
 #define PNCXK_MAXGRP 8
 typedef struct pncxk_groups {
-    int       n;
-    int       s0[PNCXK_MAXGRP];
-    long long b0[PNCXK_MAXGRP];
-    long long per[PNCXK_MAXGRP];
+    int                n;
+    int                s0[PNCXK_MAXGRP];
+    long long          b0[PNCXK_MAXGRP];
+    long long          per[PNCXK_MAXGRP];
+    unsigned long long mag[PNCXK_MAXGRP];
+    int                shr[PNCXK_MAXGRP];
 } pncxk_groups;
 
 typedef struct pncxk_batch_args {
     const pncxk_seg *dsegs;    /* device array, sorted by block0           */
     int              nseg;
     long long        nblocks;
-    long long        uniform;  /* blocks per segment if all equal, else 0  */
     int             *dmap;     /* device block->segment table or NULL      */
-    pncxk_groups     grp;      /* used when uniform == 0 and grp.n > 0     */
+    pncxk_groups     grp;      /* block -> segment runs when grp.n > 0, else dmap */
     int              sval;     /* value a segment's status word gets on ERANGE */
     void            *stream;
     void            *ev_start; /* timing events stamped at this launch's start */

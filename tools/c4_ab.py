@@ -7,7 +7,7 @@ A is the in-tree library; B is another build of the same sources, e.g.
     make -C pnetcdf_amd/csrc OUT=$PWD/tools/ab OBJ=$PWD/tools/ab/obj \\
         "HIPFLAGS=--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -DPNCX_BATCH_REMAP=0" \\
         $PWD/tools/ab/libpncx.so
-    python tools/c4_ab.py --b tools/ab/libpncx.so [--rounds 6] [--steps 20]
+    python tools/c4_ab.py --b tools/ab/libpncx.so [--b other.so] [--rounds 6] [--steps 20]
 
 Each library gets its own C4 buffers (bench.py's C4Batch: torch allocations,
 splitmix64 data) for the synchronous, asynchronous and NC_ERANGE workloads;
@@ -15,6 +15,7 @@ each sample is bench.py's measure() (kernel time from the library's
 dispatch-stamped events, call time from the wall clock).
 """
 import argparse
+import copy
 import ctypes
 import json
 import os
@@ -27,25 +28,54 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--b", required=True)
+    ap.add_argument("--b", required=True, action="append",
+                    help="another build of libpncx.so (repeatable: B, C, ...)")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--modes", default="sync,async,erange")
     a = ap.parse_args()
     import torch
     import bench
     from pnetcdf_amd import pncx
     from pnetcdf_amd.shard import Group
-    libs = {"A": pncx.lib(), "B": ctypes.CDLL(os.path.abspath(a.b), mode=ctypes.RTLD_LOCAL)}
+    # RTLD_DEEPBIND: each other build must call its own kernel launchers --
+    # without it the first library (loaded RTLD_GLOBAL) interposes every
+    # pncxk_* symbol the others call, so their host code runs A's kernels
+    libs = {"A": pncx.lib()}
+    for k, path in enumerate(a.b):
+        libs[chr(ord("B") + k)] = ctypes.CDLL(os.path.abspath(path), mode=ctypes.RTLD_LOCAL | os.RTLD_DEEPBIND)
     stream = torch.cuda.current_stream()
     sptr = ctypes.c_void_p(stream.cuda_stream)
     group = Group()
-    modes = ("sync", "async", "erange")
-    wls = {(k, m): bench.C4Batch(torch, L, sptr, m) for k, L in libs.items() for m in modes}
+    modes = tuple(a.modes.split(","))
+    # one buffer set per library and mode; in round r library k runs on the
+    # buffer set of library (k + r) mod n, so each build meets every placement
+    # (placement alone moved the same kernels by 3 % between buffer sets)
+    names = list(libs)
+    sets = {(i, m): bench.C4Batch(torch, libs["A"], sptr, m) for i in range(len(names)) for m in modes}
+
+    def view(w, L):
+        v = copy.copy(w)
+        nvar, arr = w._nvar, w._arr
+        if w._async:
+            dp = ctypes.c_void_p(w._tdst.data_ptr())
+            v.launch = lambda: bench._ok(L.pncx_dev_batch_async(arr, nvar, dp, sptr))
+        else:
+            stv = w._stv
+            v.launch = lambda: bench._ok(L.pncx_dev_batch(arr, nvar, stv, sptr),
+                                         w._T.NC_ERANGE if w._erange else 0)
+        return v
+
+    wls = {}
     res = {}
     for r in range(a.rounds):
         for m in modes:
-            for k, L in libs.items():
-                el, km, cm = bench.measure(torch, L, group, stream, wls[(k, m)], a.steps, 3)
+            for ki, (k, L) in enumerate(libs.items()):
+                wls[(k, m)] = view(sets[((ki + r) % len(names), m)], L)
+                try:
+                    el, km, cm = bench.measure(torch, L, group, stream, wls[(k, m)], a.steps, 3)
+                except AssertionError as e:
+                    raise SystemExit(f"library {k} ({m}): {e!r}")
                 assert wls[(k, m)].check(), (k, m)
                 res.setdefault((m, k), []).append((km, el * 1e3 / a.steps))
     for (m, k), v0 in sorted(res.items()):

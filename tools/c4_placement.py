@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--steady", action="store_true",
+                    help="time --reps launches back to back between two events instead of each launch alone")
     a = ap.parse_args()
     import torch
     from pnetcdf_amd import nctypes as T
@@ -110,6 +112,16 @@ def main():
         for (k, pol), arr in arrs.items():
             for _ in range(3):
                 assert lib.pncx_dev_batch_async(arr, len(arr), dp, sp) == 0
+            if a.steady:    # reps launches back to back between two events (the sweeps' method)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(a.reps):
+                    assert lib.pncx_dev_batch_async(arr, len(arr), dp, sp) == 0
+                e1.record(stream)
+                torch.cuda.synchronize()
+                if r > 0:
+                    res[(k, pol)].append(e0.elapsed_time(e1) / a.reps)
+                continue
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
             for e0, e1 in ev:
                 e0.record(stream)

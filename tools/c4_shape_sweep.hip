@@ -64,6 +64,29 @@ __global__ __launch_bounds__(L) void k_seg(const Seg *segs) {
     st(sg.dst + i, sw(__builtin_nontemporal_load(sg.src + i), sg.es));
 }
 
+// translation warm-up: the first block of each segment has one lane load a
+// word from every 2 MiB of the segment D ahead (source and destination), so
+// a TLB miss there is taken before that segment's blocks need it
+template <int L, int D>
+__global__ __launch_bounds__(L) void k_segt(const Seg *segs) {
+    constexpr long long PS = (2ll << 20) / (L * 16), PF = (4ll << 20) / (L * 16);
+    const long long t = remap(blockIdx.x, gridDim.x);
+    const int s = t < 128 * PS ? (int)(t / PS) : 128 + (int)((t - 128 * PS) / PF);
+    const Seg sg = segs[s];
+    const long long rel = t - sg.block0;
+    if (rel == 0 && threadIdx.x < 4 && s + D < 256) {
+        const Seg nx = segs[s + D];
+        const char *p = (threadIdx.x & 1) ? (const char *)nx.dst : (const char *)nx.src;
+        p += (threadIdx.x >> 1) * (2 << 20);
+        if ((threadIdx.x >> 1) * 2 < nx.es) {
+            unsigned w = __builtin_nontemporal_load((const unsigned *)p);
+            asm volatile("" ::"v"(w));
+        }
+    }
+    const long long i = rel * L + threadIdx.x;
+    st(sg.dst + i, sw(__builtin_nontemporal_load(sg.src + i), sg.es));
+}
+
 // U vectors per lane (tile = L x 16 x U bytes, each instruction one
 // contiguous L x 16 B run), all loads issued before the stores: the
 // descriptor's dependent load is paid once per U vectors
@@ -156,6 +179,9 @@ int main() {
 #define PL(L, RM) vs.push_back({"pool " #L " remap " #RM, L, 1, 1, [](const Seg *s, const u32x4 *, u32x4 *, long long nb) { \
         k_seg<L, RM><<<nb, L>>>(s); }, {}});
     PL(256, true) PL(1024, true) PL(1024, false)
+#define ST(L, D) vs.push_back({"seg  " #L " remap 1 touch" #D, L, 1, 0, [](const Seg *s, const u32x4 *, u32x4 *, long long nb) { \
+        k_segt<L, D><<<nb, L>>>(s); }, {}});
+    ST(256, 1) ST(256, 2) ST(1024, 1) ST(1024, 2)
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
