@@ -496,7 +496,7 @@ def worker(args):
         extra = {}
         for name in EXTRA:
             w = make_workload(name, torch, lib, sptr, args, world, rank)
-            el, km, cm = measure(torch, lib, group, stream, w, args.extra_steps, args.warmup)
+            el, km, cm = measure(torch, lib, group, stream, w, args.extra_steps, max(args.warmup, args.extra_warmup))
             v, mps, rf = summary(w, el, km, cm, args.extra_steps, world)
             extra[name] = {"value": round(v, 2), "unit": "GiB/s", "ms_per_step": round(mps, 4),
                            "steps": args.extra_steps, "dtype": w.dtype, "config": w.cfg, "roofline": rf,
@@ -535,6 +535,9 @@ def main(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="N=1, c2: skip the c3/c4 workloads")
     ap.add_argument("--extra-steps", type=int, default=20)
+    ap.add_argument("--extra-warmup", type=int, default=20,
+                    help="untimed calls before each extra workload's timed ones (the first ~20 batch calls "
+                         "after its buffers are made run 1-3 %% slower, tools/c4_ab.py round 0)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--async-batch", action="store_true",
                     help="c4: pncx_dev_batch_async (statuses stay in HBM, calls queue back to back) "
