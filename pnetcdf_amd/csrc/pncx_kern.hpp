@@ -260,8 +260,15 @@ template <int XT, int IT, bool P> struct may_range<PutOp<XT, IT, P>> {
 // and a 64-bit division here: 5.6 % slower than the same kernel with a
 // constant divisor on the C4 layout (tools/c4_placement.py --steady against
 // tools/c4_shape_sweep.hip, one box).
+// ONE_FIRST: test for a single run before the run scan.  Measured both ways
+// on the C4 batches (tools/c4_ab.py, rotated buffer sets): k_batch's
+// float -> NC_SHORT class (one run) 1.3-2 % faster with the test, the
+// same-type mix kernel (two runs) ~1 % slower, so only k_batch has it.
+template <bool ONE_FIRST>
 __device__ __forceinline__ int batch_segment(long long b, const int *map, const pncxk_groups &g,
                                              const pncxk_seg *segs, int nseg) {
+    if (ONE_FIRST && g.n == 1)             // all segments equal: no run to pick
+        return g.s0[0] + (int)(((unsigned long long)(b - g.b0[0]) * g.mag[0]) >> g.shr[0]);
     if (g.n > 0) {
         long long b0 = g.b0[0];
         unsigned long long mag = g.mag[0];
@@ -492,7 +499,7 @@ __global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg, 
     using S = Shape<Op>;
     __shared__ __attribute__((aligned(16))) uint8_t lds[S::USE_LDS ? 4096 : 16];
     const long long b = batch_block();   // logical block: segment lookup and flag slot
-    const int lo = batch_segment(b, map, grp, segs, nseg);
+    const int lo = batch_segment<true>(b, map, grp, segs, nseg);
     const pncxk_seg sg = segs[lo];
     const uint8_t *src = (const uint8_t *)sg.src;
     uint8_t *dst = (uint8_t *)sg.dst;

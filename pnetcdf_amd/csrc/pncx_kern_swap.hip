@@ -330,7 +330,7 @@ __global__ __launch_bounds__(MIX_LANES) void k_batch_swapmix(const pncxk_seg *se
     // tiles): 75.8-77.1 % -> 80.3-82.7 % of peak on the C4 layout at 1024
     // lanes, three boxes (tools/c4_shape_sweep.hip, profiles/r02_c4_shape_sweep*.txt)
     const long long b = batch_block();
-    const int s = batch_segment(b, map, grp, segs, nseg);
+    const int s = batch_segment<false>(b, map, grp, segs, nseg);
     const pncxk_seg sg = segs[s];
     const uint8_t *src = (const uint8_t *)sg.src;
     uint8_t *dst = (uint8_t *)sg.dst;
