@@ -534,7 +534,9 @@ def main(argv=None):
     ap.add_argument("--slab-gib", type=float, default=32.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="N=1, c2: skip the c3/c4 workloads")
-    ap.add_argument("--extra-steps", type=int, default=20)
+    ap.add_argument("--extra-steps", type=int, default=200,
+                    help="timed calls of each extra workload (20 calls of ~0.25 ms read 2-5 %% high: the rate settles "
+                         "over the first ~100, profiles/r02s_bench_x200.json)")
     ap.add_argument("--extra-warmup", type=int, default=20,
                     help="untimed calls before each extra workload's timed ones (the first ~20 batch calls "
                          "after its buffers are made run 1-3 %% slower, tools/c4_ab.py round 0)")
