@@ -816,3 +816,33 @@ def test_dev_batch_fuzz_all_pairs(torch_cuda, seed):
         assert rc in (T.NC_NOERR, T.NC_ERANGE), rc
         torch.cuda.synchronize()
         _check_refs(refs, dst.cpu().tolist())
+
+
+def test_flag_slots_many_streams(torch_cuda):
+    """NC_ERANGE flag arrays belong to one (device, stream) and there are 32
+    of them: 40 streams in turn hand slots over (the device is drained
+    first), and a larger launch regrows a slot.  Each call's status and
+    bytes must still match the oracle, with the calls of all streams queued
+    before anything is read back."""
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    ora = OracleConv()
+    rng = np.random.default_rng(0x51075)
+    streams = [torch.cuda.Stream() for _ in range(40)]
+    fill = T.fill_bytes(T.NC_SHORT)
+    checks = []
+    for n in (1 << 12, 1 << 20, 1 << 14):          # small, then regrow every slot, then small again
+        for k, s in enumerate(streams):
+            lo, hi = (-40000.0, 40000.0) if k % 3 == 0 else (-30000.0, 30000.0)
+            vals = rng.uniform(lo, hi, n).astype(np.float32)
+            di = torch.from_numpy(vals).cuda()
+            dx = torch.zeros(n * 2, dtype=torch.uint8, device="cuda")
+            ds = torch.zeros(1, dtype=torch.int32, device="cuda")
+            torch.cuda.current_stream().synchronize()        # inputs copied before the other stream reads them
+            pncx.dev_putn(5, T.NC_SHORT, dx, di, n, T.ITYPE_FLOAT, fill, ds, stream=s)
+            checks.append((vals, dx, ds, s))
+    torch.cuda.synchronize()
+    for vals, dx, ds, _s in checks:
+        exp, so = ora.putn(5, T.NC_SHORT, vals, T.ITYPE_FLOAT, fill)
+        assert int(ds.item()) == so
+        assert dx.cpu().numpy().tobytes() == exp
