@@ -7,6 +7,10 @@
 //   seq    launch order
 //   xcd    XCD-contiguous (each XCD one contiguous run of tiles, k_tile's)
 //   chunk  XCD-interleaved chunks of 64 tiles (all XCDs near each other)
+//   xcd/S  each XCD walks S sub-ranges of its range side by side (8 S streams)
+//   xcdxG  G XCDs share one range, tiles interleaved (8 / G streams)
+// Result (profiles/r02s_c2_order_sweep.txt): 8 streams (xcd, xcdx2, chunk at
+// 1024 lanes) 85.0-85.4 %; 16 / 32 streams 79.6-80.4 / 75.0-75.6 %.
 // over S GiB in place (argv[1], default 32), splitmix64 data, 10 launches
 // back to back per sample, interleaved rounds.
 #include <hip/hip_runtime.h>
@@ -39,11 +43,26 @@ __device__ __forceinline__ long long order(long long b, long long nb) {
         const long long q = nb >> 3, r = nb & 7, x = b & 7;
         return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
     }
-    // chunks of 64 tiles dealt round-robin over the 8 XCDs: block b (XCD b & 7)
-    // takes tile (b >> 3) % 64 of chunk ((b >> 3) / 64) * 8 + (b & 7); the
-    // grid is a multiple of 512 blocks here
-    const long long x = b & 7, k = b >> 3;
-    return ((k >> 6) * 8 + x) * 64 + (k & 63);
+    if constexpr (ORD == 2) {
+        // chunks of 64 tiles dealt round-robin over the 8 XCDs: block b (XCD b & 7)
+        // takes tile (b >> 3) % 64 of chunk ((b >> 3) / 64) * 8 + (b & 7); the
+        // grid is a multiple of 512 blocks here
+        const long long x = b & 7, k = b >> 3;
+        return ((k >> 6) * 8 + x) * 64 + (k & 63);
+    }
+    if constexpr (ORD == 3 || ORD == 4) {
+        // XCD-contiguous, but each XCD's range split into S = 2 / 4 sub-ranges
+        // walked side by side (8 S concurrent streams instead of 8); the grid
+        // is a multiple of 8 S blocks here
+        constexpr long long S = ORD == 3 ? 2 : 4;
+        const long long x = b & 7, k = b >> 3, per = nb >> 3;
+        return x * per + (k % S) * (per / S) + k / S;
+    }
+    // ORD = 5 / 6: G = 2 / 4 XCDs share one contiguous range (8 / G streams),
+    // their blocks interleaved tile by tile
+    constexpr long long G = ORD == 5 ? 2 : 4;
+    const long long x = b & 7, k = b >> 3, per = nb / (8 / G);
+    return (x / G) * per + k * G + (x % G);
 }
 
 template <int L, int ORD>
@@ -74,6 +93,8 @@ int main(int argc, char **argv) {
     VAR(256, 1, "xcd") VAR(512, 1, "xcd") VAR(1024, 1, "xcd")
     VAR(256, 0, "seq") VAR(1024, 0, "seq")
     VAR(256, 2, "chunk") VAR(1024, 2, "chunk")
+    VAR(256, 3, "xcd/2") VAR(1024, 3, "xcd/2")
+    VAR(256, 5, "xcdx2") VAR(256, 6, "xcdx4") VAR(1024, 5, "xcdx2") VAR(1024, 6, "xcdx4")
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
