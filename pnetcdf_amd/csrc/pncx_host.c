@@ -1228,11 +1228,11 @@ static int cmp_seg_size(const void *pa, const void *pb)
  * (pncx_shim.h): shr = 31 + ceil(log2 per), mag = ceil(2^shr / per) */
 static void group_magic(pncxk_groups *g, int k)
 {
-    const long long d = g->per[k];
+    const long long d = g->r[k].per;
     int l = 0;
     while ((1LL << l) < d) l++;
-    g->shr[k] = 31 + l;
-    g->mag[k] = ((1ULL << g->shr[k]) - 1) / (unsigned long long)d + 1;
+    g->r[k].shr = 31 + l;
+    g->r[k].mag = ((1ULL << g->r[k].shr) - 1) / (unsigned long long)d + 1;
 }
 
 /* Non-uniform class: sort its segments by block count and describe the runs
@@ -1245,11 +1245,11 @@ static int make_groups(pncxk_seg *seg, int count, pncxk_groups *g)
     qsort(seg, (size_t)count, sizeof *seg, cmp_seg_size);
     for (k = 0; k < count; k++) {
         const long long nb = seg[k].nvec > 0 ? seg[k].nvec : 1;
-        if (n == 0 || g->per[n - 1] != nb) {
+        if (n == 0 || g->r[n - 1].per != nb) {
             if (n == PNCXK_MAXGRP) return 0;
-            g->s0[n] = k;
-            g->b0[n] = b0;
-            g->per[n] = nb;
+            g->r[n].s0 = k;
+            g->r[n].b0 = b0;
+            g->r[n].per = nb;
             n++;
         }
         seg[k].block0 = b0;
@@ -1340,7 +1340,7 @@ static int batch_plan(plan_t *p)
         if (c->count > 0) {
             if (c->uniform > 0) {                  /* all equal: one run */
                 c->grp.n = 1;
-                c->grp.per[0] = c->uniform;
+                c->grp.r[0].per = c->uniform;
                 group_magic(&c->grp, 0);
                 c->map_off = -1;
             } else if (make_groups(p->seg + c->first, c->count, &c->grp)) {

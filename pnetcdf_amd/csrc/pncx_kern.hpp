@@ -254,29 +254,35 @@ template <int XT, int IT, bool P> struct may_range<PutOp<XT, IT, P>> {
 };
 
 // block -> segment of a batch grid: a few runs of equal sizes (e.g. NC_SHORT
-// and NC_FLOAT variables; all-equal is one run) pick their run with
-// independent kernarg loads and divide by a host-computed multiply + shift;
-// anything else reads the device map.  Round 2 had a dependent load per run
-// and a 64-bit division here: 5.6 % slower than the same kernel with a
-// constant divisor on the C4 layout (tools/c4_placement.py --steady against
-// tools/c4_shape_sweep.hip, one box).
-// ONE_FIRST: test for a single run before the run scan.  Measured both ways
-// on the C4 batches (tools/c4_ab.py, rotated buffer sets): k_batch's
+// and NC_FLOAT variables; all-equal is one run) divide by a host-computed
+// multiply + shift; anything else reads the device map.  One or two runs
+// (every C4 batch) read the two run records with their kernel arguments and
+// select; reading the whole 8-run table first cost the C4 mix kernel 3 points
+// of peak against constant divisors (tools/c4_kernel_ablation.hip P1 / P6 /
+// P3: 80.8 / 83.5 / 83.6 % on one pool per side).
+__device__ __forceinline__ int run_segment(long long b, const pncxk_run &r) {
+    return r.s0 + (int)(((unsigned long long)(b - r.b0) * r.mag) >> r.shr);
+}
+
+// ONE_FIRST: test for a single run first.  Measured both ways on the C4
+// batches (tools/c4_ab.py, rotated buffer sets) with the 8-run scan: k_batch's
 // float -> NC_SHORT class (one run) 1.3-2 % faster with the test, the
 // same-type mix kernel (two runs) ~1 % slower, so only k_batch has it.
 template <bool ONE_FIRST>
 __device__ __forceinline__ int batch_segment(long long b, const int *map, const pncxk_groups &g,
                                              const pncxk_seg *segs, int nseg) {
-    if (ONE_FIRST && g.n == 1)             // all segments equal: no run to pick
-        return g.s0[0] + (int)(((unsigned long long)(b - g.b0[0]) * g.mag[0]) >> g.shr[0]);
-    if (g.n > 0) {
-        long long b0 = g.b0[0];
-        unsigned long long mag = g.mag[0];
-        int shr = g.shr[0], s0 = g.s0[0];
-#pragma unroll
-        for (int k = 1; k < PNCXK_MAXGRP; k++)
-            if (k < g.n && b >= g.b0[k]) { b0 = g.b0[k]; mag = g.mag[k]; shr = g.shr[k]; s0 = g.s0[k]; }
+    if (ONE_FIRST && g.n == 1) return run_segment(b, g.r[0]);
+    if (g.n > 0 && g.n <= 2) {
+        const bool hi = g.n == 2 && b >= g.r[1].b0;
+        const long long b0 = hi ? g.r[1].b0 : g.r[0].b0;
+        const unsigned long long mag = hi ? g.r[1].mag : g.r[0].mag;
+        const int s0 = hi ? g.r[1].s0 : g.r[0].s0, shr = hi ? g.r[1].shr : g.r[0].shr;
         return s0 + (int)(((unsigned long long)(b - b0) * mag) >> shr);
+    }
+    if (g.n > 2) {
+        int k = 0;
+        while (k + 1 < g.n && b >= g.r[k + 1].b0) k++;
+        return run_segment(b, g.r[k]);
     }
     if (map != nullptr) return map[b];
     int lo = 0, hi = nseg - 1;             // binary search (sorted by block0)

@@ -37,18 +37,24 @@ typedef struct pncxk_seg {
 } pncxk_seg;
 
 /* up to PNCXK_MAXGRP runs of equal-size segments: block b of the grid is in
- * group g when b0[g] <= b < b0[g+1], segment s0[g] + (b - b0[g]) / per[g].
- * The division is a multiply and a shift: q = (r * mag[g]) >> shr[g] with
- * mag = ceil(2^shr / per), shr = 31 + ceil(log2 per), exact for r < 2^31
- * (a class grid never reaches 2^31 blocks: that would be >= 8 TiB). */
+ * run k when r[k].b0 <= b < r[k+1].b0, segment r[k].s0 + (b - r[k].b0) / r[k].per.
+ * The division is a multiply and a shift: q = (x * mag) >> shr with
+ * mag = ceil(2^shr / per), shr = 31 + ceil(log2 per), exact for x < 2^31
+ * (a class grid never reaches 2^31 blocks: that would be >= 8 TiB).  One
+ * record per run, so a kernel with one or two runs reads 64 contiguous bytes
+ * of its arguments (the C4 batches: tools/c4_kernel_ablation.hip). */
 #define PNCXK_MAXGRP 8
+typedef struct pncxk_run {
+    long long          b0;    /* first block of the run            */
+    unsigned long long mag;   /* multiplier for / per              */
+    long long          per;   /* blocks per segment in this run    */
+    int                s0;    /* first segment of the run          */
+    int                shr;   /* shift for / per                   */
+} pncxk_run;
 typedef struct pncxk_groups {
-    int                n;
-    int                s0[PNCXK_MAXGRP];
-    long long          b0[PNCXK_MAXGRP];
-    long long          per[PNCXK_MAXGRP];
-    unsigned long long mag[PNCXK_MAXGRP];
-    int                shr[PNCXK_MAXGRP];
+    int       n;
+    int       pad;
+    pncxk_run r[PNCXK_MAXGRP];
 } pncxk_groups;
 
 typedef struct pncxk_batch_args {

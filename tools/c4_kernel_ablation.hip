@@ -10,9 +10,15 @@
 //   P0  the product kernel body (group lookup, descriptor, head/tail block,
 //       4-way element-size switch)
 //   P1  P0 without the head/tail block (the C4 segments have none)
+//       (P0/P1 ran at 80.8 % on the pool with round 2's 8-run table read
+//       whole; P6 83.5 %, P3 83.6 %: the product now reads one or two run
+//       records, profiles/r02s_c4_ablation*.txt)
 //   P2  P1 with the sweep's 2-way swap (es 2 or 4)
 //   P3  P1 with the segment found by constant divisors (the sweep's rule)
 //   P4  P1 reading only src/dst/aux/block0 (no head/nvec offsets)
+//   P5  P1 with the run table read from device memory instead of the kernarg
+//   P6  P1 with two runs passed as a compact kernarg struct
+//   P7  P1 with the segment read from a device block -> segment map
 //   MIN the minimal kernel (tools/c4_shape_sweep.hip k_seg<1024, remap>)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -62,11 +68,22 @@ __device__ __forceinline__ void mix_scalar(const uint8_t *src, uint8_t *dst, int
     for (int64_t e = e0 + threadIdx.x; e < e1; e += L) scalar_elem<Op>(src, dst, e, 0, bad);
 }
 
+struct Grp2 { int n, s01; long long b01; unsigned long long mag0, mag1; int shr0, shr1; };
+
 template <int V>
-__global__ __launch_bounds__(L) void k_var(const pncxk_seg *segs, int nseg, const int *map, pncxk_groups grp) {
+__global__ __launch_bounds__(L) void k_var(const pncxk_seg *segs, int nseg, const int *map, pncxk_groups grp,
+                                           const pncxk_groups *dgrp, Grp2 g2) {
     const long long b = batch_block();
     int s;
-    if constexpr (V == 3) {
+    if constexpr (V == 5) {
+        s = batch_segment<false>(b, nullptr, *dgrp, segs, nseg);
+    } else if constexpr (V == 6) {
+        const bool hi = g2.n > 1 && b >= g2.b01;
+        const unsigned long long r = (unsigned long long)(b - (hi ? g2.b01 : 0));
+        s = (hi ? g2.s01 : 0) + (int)((r * (hi ? g2.mag1 : g2.mag0)) >> (hi ? g2.shr1 : g2.shr0));
+    } else if constexpr (V == 7) {
+        s = map[b];
+    } else if constexpr (V == 3) {
         constexpr long long PS = (2ll << 20) / (L * 16), PF = (4ll << 20) / (L * 16);
         s = b < 128 * PS ? (int)(b / PS) : 128 + (int)((b - 128 * PS) / PF);
     } else {
@@ -122,9 +139,9 @@ __global__ void k_rand(uint64_t *p, long long n, uint64_t seed) {
 
 static void magic(pncxk_groups *g, int k) {       // the host rule of pncx_host.c group_magic
     int l = 0;
-    while ((1LL << l) < g->per[k]) l++;
-    g->shr[k] = 31 + l;
-    g->mag[k] = ((1ULL << g->shr[k]) - 1) / (unsigned long long)g->per[k] + 1;
+    while ((1LL << l) < g->r[k].per) l++;
+    g->r[k].shr = 31 + l;
+    g->r[k].mag = ((1ULL << g->r[k].shr) - 1) / (unsigned long long)g->r[k].per + 1;
 }
 
 int main() {
@@ -158,10 +175,20 @@ int main() {
     }
     pncxk_groups grp{};
     grp.n = 2;
-    grp.s0[0] = 0; grp.b0[0] = 0; grp.per[0] = (2ll << 20) / (L * 16);
-    grp.s0[1] = 128; grp.b0[1] = 128 * grp.per[0]; grp.per[1] = (4ll << 20) / (L * 16);
+    grp.r[0].s0 = 0; grp.r[0].b0 = 0; grp.r[0].per = (2ll << 20) / (L * 16);
+    grp.r[1].s0 = 128; grp.r[1].b0 = 128 * grp.r[0].per; grp.r[1].per = (4ll << 20) / (L * 16);
     magic(&grp, 0);
     magic(&grp, 1);
+    pncxk_groups *dgrp;
+    CK(hipMalloc(&dgrp, sizeof grp));
+    CK(hipMemcpy(dgrp, &grp, sizeof grp, hipMemcpyHostToDevice));
+    Grp2 g2{2, 128, grp.r[1].b0, grp.r[0].mag, grp.r[1].mag, grp.r[0].shr, grp.r[1].shr};
+    std::vector<int> hmap(nb);
+    for (long long b = 0; b < nb; b++)
+        hmap[b] = b < grp.r[1].b0 ? (int)(b / grp.r[0].per) : 128 + (int)((b - grp.r[1].b0) / grp.r[0 + 1].per);
+    int *dmap;
+    CK(hipMalloc(&dmap, sizeof(int) * nb));
+    CK(hipMemcpy(dmap, hmap.data(), sizeof(int) * nb, hipMemcpyHostToDevice));
     pncxk_seg *ds[2];
     MinSeg *dm[2];
     for (int lay = 0; lay < 2; lay++) {
@@ -172,17 +199,20 @@ int main() {
     }
     struct Var { std::string n; int lay; int v; std::vector<float> ms; };
     std::vector<Var> vs;
-    const char *names[] = {"P0", "P1", "P2", "P3", "P4", "MIN"};
+    const char *names[] = {"P0", "P1", "P2", "P3", "P4", "P5", "P6", "P7", "MIN"};
     for (int lay = 0; lay < 2; lay++)
-        for (int v = 0; v < 6; v++) vs.push_back({std::string(lay ? "sep  " : "pool ") + names[v], lay, v, {}});
+        for (int v = 0; v < 9; v++) vs.push_back({std::string(lay ? "sep  " : "pool ") + names[v], lay, v, {}});
     auto run = [&](const Var &v) {
         const pncxk_seg *s = ds[v.lay];
         switch (v.v) {
-            case 0: k_var<0><<<nb, L>>>(s, 256, nullptr, grp); break;
-            case 1: k_var<1><<<nb, L>>>(s, 256, nullptr, grp); break;
-            case 2: k_var<2><<<nb, L>>>(s, 256, nullptr, grp); break;
-            case 3: k_var<3><<<nb, L>>>(s, 256, nullptr, grp); break;
-            case 4: k_var<4><<<nb, L>>>(s, 256, nullptr, grp); break;
+            case 0: k_var<0><<<nb, L>>>(s, 256, nullptr, grp, dgrp, g2); break;
+            case 1: k_var<1><<<nb, L>>>(s, 256, nullptr, grp, dgrp, g2); break;
+            case 2: k_var<2><<<nb, L>>>(s, 256, nullptr, grp, dgrp, g2); break;
+            case 3: k_var<3><<<nb, L>>>(s, 256, nullptr, grp, dgrp, g2); break;
+            case 4: k_var<4><<<nb, L>>>(s, 256, nullptr, grp, dgrp, g2); break;
+            case 5: k_var<5><<<nb, L>>>(s, 256, nullptr, grp, dgrp, g2); break;
+            case 6: k_var<6><<<nb, L>>>(s, 256, nullptr, grp, dgrp, g2); break;
+            case 7: k_var<7><<<nb, L>>>(s, 256, dmap, grp, dgrp, g2); break;
             default: k_min<<<nb, L>>>(dm[v.lay]); break;
         }
     };
