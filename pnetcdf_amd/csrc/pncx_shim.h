@@ -25,15 +25,18 @@ typedef struct pncxk_args {
 
 /* one segment of a batched launch (device-resident copy of this array) */
 typedef struct pncxk_seg {
+    /* what every block of a batch kernel reads first: one 64-byte line */
     const void        *src;
     void              *dst;
-    long long          n;
     long long          head;   /* scalar elements before the 16B-aligned body */
     long long          nvec;   /* vector steps in the body                    */
     long long          block0; /* first block of this segment                 */
     unsigned long long fill;
-    int               *status; /* device int of this segment, or NULL         */
     int                aux;    /* SWAPMIX: element size of this segment       */
+    int                pad;
+    /* the segment's first block (head/remainder) and the flag reduce */
+    long long          n;
+    int               *status; /* device int of this segment, or NULL         */
 } pncxk_seg;
 
 /* up to PNCXK_MAXGRP runs of equal-size segments: block b of the grid is in
