@@ -323,8 +323,9 @@ int pncx_dev_batch_async(const pncx_seg *segs, int nseg, int *dstatus,
 /* Measurement aid (no reference counterpart): with timing enabled, every
  * pncx_dev_batch and pncx_dev_batch_async call on the current device has
  * its batch kernels stamped with HIP events by their own dispatches (start
- * of the first class kernel, end of the last; not the descriptor upload,
- * the status copy or the wait).  pncx_dev_batch_kernel_ms waits for the
+ * and end of every class kernel, summed per call; not the descriptor
+ * upload, the flag reduce, the status copy or the wait).  A call with more
+ * than 256 classes is not timed.  pncx_dev_batch_kernel_ms waits for the
  * calls still queued and returns the summed kernel time and the number of
  * calls timed since pncx_dev_batch_timing(1) (which resets both). */
 int pncx_dev_batch_timing(int enable);
