@@ -1384,9 +1384,14 @@ static void batch_time_drain(ctx_t *c)
     c->tpend = c->tcpend = 0;
 }
 
-/* the call whose launches used the c->tnext pairs after tpend has completed */
+/* the call whose launches used the c->tnext pairs after tpend has completed
+ * (tnext < 0: a call with more classes than the ring holds, not timed) */
 static void batch_time(ctx_t *c)
 {
+    if (c->tnext < 0) {
+        c->tnext = 0;
+        return;
+    }
     c->tpend += c->tnext;
     c->tnext = 0;
     c->tcpend++;
@@ -1407,7 +1412,7 @@ static int launch_classes(const cls_t *cls, int ncls, uint8_t *dbase, size_t sof
      * timed.  A call with more classes than the event ring holds goes untimed. */
     const int timed = tc != NULL && tc->timing && ncls <= NTEV;
     if (timed && tc->tpend + ncls > NTEV) batch_time_drain(tc);
-    if (tc != NULL) tc->tnext = 0;
+    if (tc != NULL) tc->tnext = tc->timing && !timed ? -1 : 0;
     pncxk_seg *dseg = (pncxk_seg *)(dbase + soff);
     int *dmap = (int *)(dbase + moff);
     for (k = 0; k < ncls && !err; k++) {
