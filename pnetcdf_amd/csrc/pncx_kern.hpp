@@ -413,16 +413,23 @@ __device__ __forceinline__ void tile_body(const uint8_t *src, uint8_t *dst, type
     } else if constexpr (SS < DS) {
         // widening: narrow src 16 B/lane -> LDS -> R wide 16 B chunks per lane
         constexpr int R = S::R, E2 = S::E2;
+        using NV = typename VecT<E2 * SS>::type;
         const auto v = ldv<16, NT>(src + lane * 16);
         *reinterpret_cast<typename VecT<16>::type *>(lds + lane * 16) = v;
         __syncthreads();
+        // all R LDS reads before the first store: the streaming store is an
+        // asm statement with a memory clobber, so reads after it cannot be
+        // hoisted by the compiler (it issued read, wait, convert, store R
+        // times in a row)
+        NV w[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) w[k] = *reinterpret_cast<const NV *>(lds + (k * 256 + lane) * E2 * SS);
 #pragma unroll
         for (int k = 0; k < R; k++) {
             const int c = k * 256 + lane;                      // wide chunk index
             alignas(16) uint8_t sb[E2 * SS];
             alignas(16) uint8_t db[16];
-            const auto w = *reinterpret_cast<const typename VecT<E2 * SS>::type *>(lds + c * E2 * SS);
-            __builtin_memcpy(sb, &w, E2 * SS);
+            __builtin_memcpy(sb, &w[k], E2 * SS);
             conv_regs<Op, E2>(sb, db, fill, bad);
             typename VecT<16>::type o;
             __builtin_memcpy(&o, db, 16);
