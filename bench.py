@@ -73,12 +73,12 @@ def launch_ranks(nproc, argv):
 
 
 # --------------------------------------------------------------- helpers
-def splitmix64_fill(torch, out, seed, chunk=1 << 27):
-    """element i = splitmix64(seed + (i+1)*golden), generated on the GPU."""
+def splitmix64_fill(torch, out, seed, chunk=1 << 27, base=0):
+    """element i = splitmix64(seed + (base+i+1)*golden), generated on the GPU."""
     n = out.numel()
     for s in range(0, n, chunk):
         m = min(chunk, n - s)
-        z = torch.arange(s + 1, s + 1 + m, dtype=torch.int64, device=out.device)
+        z = torch.arange(base + s + 1, base + s + 1 + m, dtype=torch.int64, device=out.device)
         z.mul_(-7046029254386353131).add_(seed)
         z = (z ^ ((z >> 30) & 0x3FFFFFFFF)) * -4658895280553007687
         z = (z ^ ((z >> 27) & 0x1FFFFFFFFF)) * -7723592293110705685
@@ -163,21 +163,82 @@ def cpu_baseline_swap8_threads(budget_s=4.0, slab_bytes=2 << 30, threads=None):
                       f"in {el:.1f} s (orc_in_swapn, gcc -O2)"}
 
 
-def cpu_baseline_getn(xtype, itype, xsz, isz, budget_s=3.0, n=1 << 26, seed=0):
-    """1-core oracle getn (ncmpii_getn_NC_<X>) on a bounded host sample."""
-    from oracle import oracle as O
-    lib = O.lib()
-    xb = np.frombuffer(np.random.default_rng(seed).bytes(n * xsz), np.uint8).copy()
-    ib = np.empty(n * isz, np.uint8)
-    passes, t0 = 0, time.perf_counter()
-    while True:
-        lib.orc_getn(5, xtype, xb.ctypes.data, ib.ctypes.data, n, itype)
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    return {"value": round((xsz + isz) * n * passes / el / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{n} elements, {passes} orc_getn passes in {el:.1f} s (gcc -O2, 1 thread)"}
+def cpu_run(jobs, threads, budget_s):
+    """Time a list of (ctypes call, algorithmic bytes) jobs on `threads` host
+    threads: thread k runs jobs k, k+T, ... over and over until the budget
+    is spent (ctypes releases the GIL inside each call).  Returns
+    (GiB/s moved, jobs completed, seconds)."""
+    import threading
+    done = [0] * threads
+    moved = [0.0] * threads
+    t_end = time.perf_counter() + budget_s
+
+    def work(k):
+        mine = jobs[k::threads]
+        while mine and time.perf_counter() < t_end:
+            for call, nbytes in mine:
+                call()
+                done[k] += 1
+                moved[k] += nbytes
+    for call, _ in jobs[:threads]:     # warm: first touch of the host pages
+        call()
+    ths = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    el = time.perf_counter() - t0
+    return sum(moved) / el / GIB, sum(done), el
+
+
+def cpu_baseline_jobs(name, jobs, threads, budget_s, sample):
+    v, calls, el = cpu_run(jobs, threads, budget_s)
+    return {"value": round(v, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{sample}; {calls} oracle calls in {el:.1f} s on {threads} thread(s) "
+                      f"(oracle/pncx_oracle.c, gcc -O2)"}
+
+
+def cpu_c3_jobs(lib, n=1 << 26, pieces=16, seed=0):
+    """NC_INT -> double getn (ncmpii_getn_NC_INT, ncx.m4:2429-2495) on a
+    2^26-element host sample cut into `pieces` disjoint slices."""
+    from pnetcdf_amd import nctypes as T
+    xb = np.frombuffer(np.random.default_rng(seed).bytes(n * 4), np.uint8).copy()
+    ib = np.empty(n * 8, np.uint8)
+    per = n // pieces
+    jobs = []
+    for k in range(pieces):
+        xp, ip = xb.ctypes.data + k * per * 4, ib.ctypes.data + k * per * 8
+        jobs.append((lambda xp=xp, ip=ip: lib.orc_getn(5, T.NC_INT, xp, ip, per, T.ITYPE_DOUBLE), 12.0 * per))
+    return jobs, (xb, ib)
+
+
+def cpu_c4_jobs(lib, erange, nel=1 << 20, nvar=256, seed=0):
+    """The C4 batch on the host: one ncmpii_putn_NC_<X> per iput request
+    (ncmpio_i_getput.m4:238-239 -> convert_swap.m4:202-330): 128 NC_SHORT
+    (from short, or from float in [-40000, 40000] for the secondary
+    variant, with the NC_SHORT fill) and 128 NC_FLOAT same-type requests of
+    2^20 elements, the whole workload in host memory."""
+    from pnetcdf_amd import nctypes as T
+    rng = np.random.default_rng(seed)
+    keep, jobs = [], []
+    fill = np.frombuffer(T.fill_bytes(T.NC_SHORT) + b"\0" * 8, np.uint8).copy()
+    keep.append(fill)
+    for v in range(nvar):
+        if v % 2 == 0 and erange:
+            ib = rng.uniform(-40000.0, 40000.0, nel).astype(np.float32)
+            xt, it, isz, xsz = T.NC_SHORT, T.ITYPE_FLOAT, 4, 2
+        elif v % 2 == 0:
+            ib = np.frombuffer(rng.bytes(nel * 2), np.int16).copy()
+            xt, it, isz, xsz = T.NC_SHORT, T.ITYPE_SHORT, 2, 2
+        else:
+            ib = np.frombuffer(rng.bytes(nel * 4), np.float32).copy()
+            xt, it, isz, xsz = T.NC_FLOAT, T.ITYPE_FLOAT, 4, 4
+        xb = np.empty(nel * xsz, np.uint8)
+        keep += [ib, xb]
+        jobs.append((lambda xt=xt, it=it, xp=xb.ctypes.data, ip=ib.ctypes.data:
+                     lib.orc_putn(5, xt, xp, ip, nel, it, fill.ctypes.data), float((isz + xsz) * nel)))
+    return jobs, keep
 
 
 def gather_leg(torch, group, buf, gib, chunk_gib, to_cpu=False):
@@ -252,9 +313,16 @@ class C2Swap(Workload):
         nrec_total = (n // rec_elems) * world
         first_rec, my_recs = record_slab(nrec_total, world, rank)
         self._tbuf = torch.empty(n, dtype=torch.int64, device="cuda")
-        splitmix64_fill(torch, self._tbuf, SEEDS["c5" if world > 1 else "c2"] + first_rec)
+        self._seed = SEEDS["c5" if world > 1 else "c2"] + first_rec
+        splitmix64_fill(torch, self._tbuf, self._seed)
         ptr = ctypes.c_void_p(self._tbuf.data_ptr())
-        self.launch = lambda: _ok(lib.pncx_dev_in_swapn(ptr, n, 8, sptr))
+        self.passes = 0
+
+        def launch():
+            _ok(lib.pncx_dev_in_swapn(ptr, n, 8, sptr))
+            self.passes += 1
+        self.launch = launch
+        self._torch, self._n = torch, n
         self.elems, self.bytes_per_elem, self.slab_per_elem = n, 16, 8
         self.metric_key, self.dtype = "swap8", "u64"
         self.kernel = "k_tile<SwapOp<8>, true>"
@@ -264,6 +332,28 @@ class C2Swap(Workload):
                     "slab_gib_per_gpu": slab_gib, "elements_per_gpu": n, "xtype": "NC_DOUBLE",
                     "itype": "double", "records_per_gpu": my_recs,
                     "parallelism": f"records sharded one slab per GPU x{world}, no data-path collective"}
+
+
+    def check(self):
+        """Every element: the in-place swap is an involution, so after an
+        odd number of passes element i is the byte reversal of the
+        splitmix64 value the slab was filled with, after an even number the
+        value itself.  The expected slab is regenerated on the GPU in 1 GiB
+        chunks and byte-reversed by torch (flip of the 8 bytes), independent
+        of the kernel under test."""
+        torch = self._torch
+        odd = self.passes % 2 == 1
+        chunk = 1 << 27
+        for s in range(0, self._n, chunk):
+            m = min(chunk, self._n - s)
+            exp = torch.empty(m, dtype=torch.int64, device="cuda")
+            splitmix64_fill(torch, exp, self._seed, base=s)
+            if odd:
+                exp = exp.view(torch.uint8).view(m, 8).flip(1).contiguous().view(torch.int64).view(m)
+            if not torch.equal(exp, self._tbuf[s:s + m]):
+                return False
+            del exp
+        return True
 
 
 class C3IntDouble(Workload):
@@ -285,13 +375,19 @@ class C3IntDouble(Workload):
         self._torch = torch
 
     def check(self):
-        """int->double is exact and never ERANGE: sampled elements equal the
-        byte-reversed int32 of the input, the status word stays NC_NOERR"""
+        """int->double is exact and never ERANGE: every element equals the
+        byte-reversed int32 of the input (torch byte flip + cast, 2^27
+        elements at a time), and the status word stays NC_NOERR"""
         torch = self._torch
-        idx = torch.randint(0, self._n, (4096,), device="cuda")
-        xi = self._txb.view(torch.int32)[idx]
-        b = xi.view(torch.uint8).view(-1, 4).flip(1).contiguous().view(torch.int32).view(-1)
-        return bool(torch.equal(b.to(torch.float64), self._tib[idx])) and int(self._tst.item()) == 0
+        xi = self._txb.view(torch.int32)
+        chunk = 1 << 27
+        for s in range(0, self._n, chunk):
+            m = min(chunk, self._n - s)
+            b = xi[s:s + m].view(torch.uint8).view(m, 4).flip(1).contiguous().view(torch.int32).view(m)
+            if not torch.equal(b.to(torch.float64), self._tib[s:s + m]):
+                return False
+            del b
+        return int(self._tst.item()) == 0
 
 
 class C4Batch(Workload):
@@ -348,11 +444,31 @@ class C4Batch(Workload):
                     else "pncx_dev_batch (statuses to host, synchronous)"}
 
     def check(self):
-        T = self._T
+        """Statuses (NC_ERANGE exactly on the float -> NC_SHORT variables of
+        the secondary variant) and every output element: a same-type
+        variable is its input with each element's bytes reversed; a float
+        -> NC_SHORT variable is trunc(x) big-endian, or the NC_SHORT fill
+        -32767 where x is outside [-32768, 32767] (NCX_PUT1F, ncx.m4:604-625;
+        computed here by torch, independent of the kernels)"""
+        T, torch = self._T, self._torch
         exp = [T.NC_ERANGE if (self._erange and v % 2 == 0) else 0 for v in range(self._nvar)]
-        if self._async:
-            return self._tdst.cpu().tolist() == exp
-        return list(self._stv) == exp
+        got = self._tdst.cpu().tolist() if self._async else list(self._stv)
+        if got != exp:
+            return False
+        for v in range(self._nvar):
+            ib, xb = self._tkeep[2 * v], self._tkeep[2 * v + 1]
+            if v % 2 == 0 and self._erange:
+                f = ib
+                o = (f > 32767.0) | (f < -32768.0)
+                want = torch.where(o, torch.full_like(f, -32767.0), f).to(torch.int32).to(torch.int16)
+                esz = 2
+            else:
+                esz = 2 if v % 2 == 0 else 4
+                want = ib
+            w = want.contiguous().view(torch.uint8).view(-1, esz).flip(1).contiguous().view(-1)
+            if not torch.equal(w, xb):
+                return False
+        return True
 
 
 def _ok(rc, allowed=0):
@@ -428,6 +544,34 @@ def summary(wl, elapsed, kern_ms, call_ms, steps, world):
     if call_ms is not None:
         roof["call_ms_avg"] = round(call_ms, 4)
     return value, elapsed * 1e3 / steps, roof
+
+
+def add_cpu_baselines(wls, budget):
+    """1-core and 16-core oracle baselines beside the other 1-GPU configs
+    (north_star: the reference's CPU swap/convert on the GPU box's own host
+    cores in the same run; 16 = the host-core share of one GPU on the box)."""
+    from oracle import oracle as O
+    lib = O.lib()
+    cores = min(16, os.cpu_count() or 1)
+    if "c3" in wls:
+        jobs, keep = cpu_c3_jobs(lib, seed=SEEDS["c3"])
+        smp = "2^26 NC_INT -> double host sample in 16 slices (orc_getn)"
+        wls["c3"]["cpu_baseline"] = cpu_baseline_jobs("c3", jobs, 1, budget, smp)
+        wls["c3"]["cpu_baseline_all_cores"] = cpu_baseline_jobs("c3", jobs, cores, budget, smp)
+        del jobs, keep
+    for name, erange in (("c4", False), ("c4_erange", True)):
+        if name not in wls:
+            continue
+        jobs, keep = cpu_c4_jobs(lib, erange, seed=SEEDS["c4"])
+        smp = ("the whole C4 secondary workload in host memory: 128 float -> NC_SHORT (~18 % NC_ERANGE + fill) "
+               "+ 128 NC_FLOAT putn of 2^20 elements" if erange else
+               "the whole C4 workload in host memory: 128 NC_SHORT + 128 NC_FLOAT same-type putn of 2^20 elements")
+        one = cpu_baseline_jobs(name, jobs, 1, budget, smp)
+        allc = cpu_baseline_jobs(name, jobs, cores, budget, smp)
+        targets = [name] + (["c4_async"] if name == "c4" and "c4_async" in wls else [])
+        for t in targets:
+            wls[t]["cpu_baseline"], wls[t]["cpu_baseline_all_cores"] = one, allc
+        del jobs, keep
 
 
 def worker(args):
@@ -511,9 +655,7 @@ def worker(args):
             line["cpu_baseline"] = cpu_baseline_swap8(args.cpu_budget)
             line["cpu_baseline_all_cores"] = cpu_baseline_swap8_threads()
             if "workloads" in line:
-                from pnetcdf_amd import nctypes as T
-                line["workloads"]["c3"]["cpu_baseline"] = cpu_baseline_getn(T.NC_INT, T.ITYPE_DOUBLE, 4, 8,
-                                                                            seed=SEEDS["c3"])
+                add_cpu_baselines(line["workloads"], args.cpu_budget_extra)
         else:
             line["cpu_baseline"] = None
         if gather is not None:
@@ -541,6 +683,8 @@ def main(argv=None):
                     help="untimed calls before each extra workload's timed ones (the first ~20 batch calls "
                          "after its buffers are made run 1-3 %% slower, tools/c4_ab.py round 0)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-budget-extra", type=float, default=3.0,
+                    help="seconds of each 1-core / all-core CPU baseline of the c3/c4 workloads")
     ap.add_argument("--async-batch", action="store_true",
                     help="c4: pncx_dev_batch_async (statuses stay in HBM, calls queue back to back) "
                          "instead of the synchronous pncx_dev_batch")

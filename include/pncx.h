@@ -348,6 +348,10 @@ int  pncx_get_device(void);
  * PNCX_EDEVICE.  Unregister before freeing the memory. */
 int  pncx_host_register(void *buf, pncx_offset nbytes);
 int  pncx_host_unregister(void *buf);
+/* 1 if p points into device memory (hipMalloc), else 0.  The file layer
+ * (pncx_nc.h) and so the ncmpi_* API take such user buffers on the
+ * device-resident path: converted in HBM, external bytes across PCIe once. */
+int  pncx_is_device_ptr(const void *p);
 /* Synchronise `stream` and return *dstatus (NC_NOERR if it was 0). */
 int  pncx_dev_status_read(const int *dstatus, pncx_stream_t stream);
 const char *pncx_strerror(int err);

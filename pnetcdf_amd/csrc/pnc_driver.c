@@ -21,9 +21,9 @@
  * 39-101); the other ranks' handles are created with
  * pncx_nc_create_shared(writer = 0) after rank 0 has created the file.
  * numrecs is made consistent with MPI_Allreduce(MAX) after every collective
- * put on a file with record variables, at collective waits, at
- * end_indep_data, sync and close (ncmpio_getput.m4:289-311,
- * ncmpio_file_misc.c:206-216).  Data goes from each rank straight to its own
+ * put of a record variable, and written when it grows (ncmpio_getput.m4:
+ * 272-311), at collective waits (ncmpio_wait.c:603-672), at end_indep_data,
+ * sync and close (ncmpio_file_misc.c:206-216).  Data goes from each rank straight to its own
  * byte ranges of the file (POSIX I/O); there is no MPI-IO and no intra-node
  * aggregation, and so no data-path collective.
  */
@@ -97,9 +97,10 @@ static MPI_Offset my_numrecs(NCM *m)
 static int sync_numrecs_mem(NCM *m)
 {
     MPI_Offset n, mx;
-    int nrec, nfix;
+    int unlim = -1;
     if (m->nprocs == 1) return NC_NOERR;
-    if (num_rec_vars(m, &nrec, &nfix) != NC_NOERR || nrec == 0) return NC_NOERR;
+    /* every rank holds the same header, so all agree whether to reduce */
+    if (pncx_nc_inq(m->ncid, NULL, NULL, NULL, &unlim) != NC_NOERR || unlim < 0) return NC_NOERR;
     n = my_numrecs(m);
     if (MPI_Allreduce(&n, &mx, 1, MPI_OFFSET, MPI_MAX, m->comm) != MPI_SUCCESS) return NC_EMPI;
     return pncx_nc_set_numrecs(m->ncid, mx);
@@ -253,6 +254,7 @@ static NCM *new_ncm(MPI_Comm comm, const char *path, int pub, MPI_Info info)
 {
     NCM *m = (NCM *)calloc(1, sizeof *m);
     if (m == NULL) return NULL;
+    m->ncid = -1;              /* pncx_nc ids start at 0: -1 = no handle yet */
     m->comm = comm;
     m->pub = pub;
     MPI_Comm_rank(comm, &m->rank);
@@ -289,7 +291,17 @@ static int drv_create(MPI_Comm comm, const char *path, int cmode, int ncid, int 
     if (root_err != NC_NOERR) { free_ncm(m); return root_err; }
     if (m->rank > 0) err = pncx_nc_create_shared(path, cmode, 0, &m->ncid);
     if ((err = min_err(m, err)) != NC_NOERR) {
-        pncx_nc_close(m->ncid);
+        /* the create failed on some rank: every rank drops its handle
+         * without writing (no header, no numrecs) and rank 0 removes the
+         * file it created, as ncmpio_abort does for a file still in its
+         * first define mode; a rank whose own create failed has no handle
+         * (m->ncid < 0) and must not close the unrelated file holding id 0 */
+        if (m->ncid >= 0) {
+            pncx_nc_set_writer(m->ncid, 0);
+            pncx_nc_close(m->ncid);
+        }
+        barrier(m);
+        if (m->rank == 0) unlink(path);
         free_ncm(m);
         return err;
     }
@@ -311,7 +323,10 @@ static int drv_open(MPI_Comm comm, const char *path, int omode, int ncid, int en
     err = pncx_nc_open(path, omode, &m->ncid);
     if (err == NC_NOERR && m->rank > 0) err = pncx_nc_set_writer(m->ncid, 0);
     if ((err = min_err(m, err)) != NC_NOERR) {
-        pncx_nc_close(m->ncid);
+        if (m->ncid >= 0) {              /* opened here, failed elsewhere: drop it unwritten */
+            pncx_nc_set_writer(m->ncid, 0);
+            pncx_nc_close(m->ncid);
+        }
         free_ncm(m);
         return err;
     }
@@ -661,10 +676,33 @@ static int drv_rename_var(void *ncp, int varid, const char *name)
 /* ------------------------------------------------------------------------ */
 /* data                                                                      */
 /* ------------------------------------------------------------------------ */
-/* after a collective put: numrecs agreed by all ranks (ncmpio_getput.m4:289-311) */
-static void coll_put_done(NCM *m, int reqMode)
+/* does varid run along the unlimited dimension (IS_RECVAR) */
+static int is_recvar(NCM *m, int varid)
 {
-    if ((reqMode & NC_REQ_COLL) && (reqMode & NC_REQ_WR)) sync_numrecs_mem(m);
+    int unlim = -1, ndims = 0, *dimids, rec;
+    if (pncx_nc_inq(m->ncid, NULL, NULL, NULL, &unlim) != NC_NOERR || unlim < 0) return 0;
+    if (pncx_nc_inq_var(m->ncid, varid, NULL, NULL, &ndims, NULL, NULL) != NC_NOERR || ndims <= 0) return 0;
+    dimids = (int *)malloc(sizeof(int) * (size_t)ndims);
+    if (dimids == NULL) return 0;
+    rec = pncx_nc_inq_var(m->ncid, varid, NULL, NULL, NULL, dimids, NULL) == NC_NOERR && dimids[0] == unlim;
+    free(dimids);
+    return rec;
+}
+
+/* After a collective put of a record variable (ncmpio_getput.m4:272-311):
+ * the MAX of every rank's record count, and if that grew past the count
+ * all ranks agreed on before the put, the new value is written to the file
+ * now (ncmpio_write_numrecs, :307; rank 0 is the writer).  Fixed-size
+ * variables and independent puts touch nothing here (independent puts
+ * are synced at the next collective call, :312-320). */
+static int coll_put_done(NCM *m, int varid, int reqMode, MPI_Offset before)
+{
+    MPI_Offset n, mx;
+    if (!(reqMode & NC_REQ_COLL) || !(reqMode & NC_REQ_WR) || !is_recvar(m, varid)) return NC_NOERR;
+    n = mx = my_numrecs(m);
+    if (m->nprocs > 1 && MPI_Allreduce(&n, &mx, 1, MPI_OFFSET, MPI_MAX, m->comm) != MPI_SUCCESS) return NC_EMPI;
+    if (before < mx) return pncx_nc_sync_numrecs(m->ncid, mx);
+    return NC_NOERR;
 }
 
 static int drv_put_var(void *ncp, int varid, const MPI_Offset *start, const MPI_Offset *count,
@@ -672,15 +710,16 @@ static int drv_put_var(void *ncp, int varid, const MPI_Offset *start, const MPI_
                        MPI_Datatype buftype, int reqMode)
 {
     NCM *m = (NCM *)ncp;
-    int err = NC_NOERR, it;
+    int err = NC_NOERR, it, e2;
+    const MPI_Offset before = my_numrecs(m);
     if (!(reqMode & NC_REQ_ZERO)) {
         if (direct_itype(m, varid, bufcount, buftype, &it) && (bufcount == -1 || buftype == MPI_DATATYPE_NULL))
             err = pncx_nc_put_varm(m->ncid, varid, start, count, stride, imap, buf, it);
         else
             err = pncx_ncmpi_put_varm(m->ncid, varid, start, count, stride, imap, buf, bufcount, buftype);
     }
-    coll_put_done(m, reqMode);
-    return err;
+    e2 = coll_put_done(m, varid, reqMode, before);
+    return (err == NC_NOERR || err == NC_ERANGE) && e2 != NC_NOERR ? e2 : err;
 }
 
 static int drv_get_var(void *ncp, int varid, const MPI_Offset *start, const MPI_Offset *count,
@@ -708,6 +747,9 @@ static int varn_buffer(NCM *m, int varid, int num, MPI_Offset *const *counts, co
         if (bufcount != -1 && buftype != MPI_DATATYPE_NULL && bufcount != want) return NC_EIOMISMATCH;
         return NC_NOERR;
     }
+    /* a derived buftype over a buffer in HBM would need a device-side
+     * MPI_Pack (the MPI library here is not GPU-aware) */
+    if (pncx_is_device_ptr(buf)) return NC_ENOTSUPPORT;
     {
         int err = pack_flex(buf, bufcount, buftype, want, pack, tmp, itype);
         if (err) return err;
@@ -720,17 +762,18 @@ static int drv_put_varn(void *ncp, int varid, int num, MPI_Offset *const *starts
                         const void *buf, MPI_Offset bufcount, MPI_Datatype buftype, int reqMode)
 {
     NCM *m = (NCM *)ncp;
-    int err = NC_NOERR, it;
+    int err = NC_NOERR, it, e2;
     void *tmp = NULL;
     const void *ptr;
+    const MPI_Offset before = my_numrecs(m);
     if (!(reqMode & NC_REQ_ZERO)) {
         err = varn_buffer(m, varid, num, counts, buf, bufcount, buftype, 1, &tmp, &ptr, &it);
         if (!err) err = pncx_nc_put_varn(m->ncid, varid, num, (const pncx_offset *const *)starts,
                                          (const pncx_offset *const *)counts, ptr, it);
         free(tmp);
     }
-    coll_put_done(m, reqMode);
-    return err;
+    e2 = coll_put_done(m, varid, reqMode, before);
+    return (err == NC_NOERR || err == NC_ERANGE) && e2 != NC_NOERR ? e2 : err;
 }
 
 static int drv_get_varn(void *ncp, int varid, int num, MPI_Offset *const *starts, MPI_Offset *const *counts,
@@ -788,9 +831,17 @@ static int drv_bput_var(void *ncp, int varid, const MPI_Offset *start, const MPI
     if (direct_itype(m, varid, bufcount, buftype, &it) &&
         (bufcount == -1 || buftype == MPI_DATATYPE_NULL || it != 0)) {
         if (it == 0) return NC_EBADTYPE;
+        if (bufcount != -1 && buftype != MPI_DATATYPE_NULL) {
+            /* a predefined buftype with an explicit bufcount must cover the
+             * request exactly (ncmpio_i_getput.m4:216, dtype_decode.c:690) */
+            pncx_nc_inq_var(m->ncid, varid, NULL, NULL, &ndims, NULL, NULL);
+            for (d = 0; d < ndims; d++) want *= count[d];
+            if (bufcount != want) return NC_EIOMISMATCH;
+        }
         return pncx_nc_bput_varm(m->ncid, varid, start, count, stride, imap, buf, it, reqid);
     }
     /* derived buftype: packed now, converted into the attached buffer now */
+    if (pncx_is_device_ptr(buf)) return NC_ENOTSUPPORT;     /* see varn_buffer */
     pncx_nc_inq_var(m->ncid, varid, NULL, NULL, &ndims, NULL, NULL);
     for (d = 0; d < ndims; d++) want *= count[d];
     if ((err = pack_flex(buf, bufcount, buftype, want, 1, &tmp, &it)) != NC_NOERR) return err;
@@ -868,6 +919,7 @@ static int drv_wait(void *ncp, int num, int *reqids, int *statuses, int reqMode)
     NCM *m = (NCM *)ncp;
     const int coll = !(reqMode & NC_REQ_INDEP);
     int err, e2, *ids = NULL;
+    MPI_Offset before;
     if (m->indef) return NC_EINDEFINE;
     if (!coll && !m->indep) return NC_ENOTINDEP;
     if (coll && m->indep) return NC_EINDEP;
@@ -877,13 +929,22 @@ static int drv_wait(void *ncp, int num, int *reqids, int *statuses, int reqMode)
         if (ids == NULL) return NC_ENOMEM;
         memcpy(ids, reqids, sizeof(int) * (size_t)num);
     }
+    before = my_numrecs(m);
     err = (num == 0) ? NC_NOERR : pncx_nc_wait_all(m->ncid, num, reqids, statuses);
     if (m->nstage > 0 && (num < 0 || ids != NULL)) {
         e2 = finish_stages(m, num, ids, 1);
         if (err == NC_NOERR) err = e2;
     }
     free(ids);
-    if (coll) sync_numrecs_mem(m);
+    if (coll) {
+        /* the MAX record count over ranks, written to the file when the
+         * flush created records (ncmpio_wait.c:603-672) */
+        sync_numrecs_mem(m);
+        if (!m->rdonly && my_numrecs(m) > before) {
+            e2 = pncx_nc_sync_numrecs(m->ncid, my_numrecs(m));
+            if (err == NC_NOERR) err = e2;
+        }
+    }
     return err;
 }
 

@@ -157,6 +157,61 @@ __device__ __forceinline__ bool in_range(S v, long long lo, unsigned long long h
     }
 }
 
+// ---------------------------------------------------------------------------
+// float (NC_FLOAT / itype float) -> integer on the float itself.  The
+// reference widens to double and casts (NCX_GET1F / NCX_PUT1F, ncx.m4:
+// 503-527, 604-625); for a float source both the range test and the x86 cast
+// are decided exactly by the float's value, so the f64 detour (and, for the
+// 64-bit targets, LLVM's f64 -> i64 expansion with its branches) is replaced
+// by float compares and integer arithmetic on the bits.  Round 2 measured
+// the detour at 66-70 % of peak for float <-> (u)int64 against 82-84 % for
+// the other 4 <-> 8 byte pairs (profiles/r03a_pmc_pairs.txt: ~100 VALU and
+// ~100 SALU instructions per wave, against 18 / 40 for NC_INT -> double).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool f32_isnan(uint32_t b) { return (b & 0x7fffffffu) > 0x7f800000u; }
+
+// |trunc(x)| for a float with |x| < 2^64 (biased exponent <= 190)
+__device__ __forceinline__ uint64_t f32_trunc_mag(uint32_t b) {
+    const int e = (int)((b >> 23) & 0xffu);
+    const uint32_t m = (b & 0x7fffffu) | 0x800000u;        // x = m * 2^(e - 150)
+    const int sh = e - 150;
+    const uint64_t up = (uint64_t)m << (sh & 63);
+    const int rs = -sh < 31 ? -sh : 31;                      // m < 2^24: >= 24 gives 0
+    const uint32_t dn = m >> (rs & 31);
+    return sh >= 0 ? up : (uint64_t)dn;
+}
+
+// x86_cast<T>((double)x) for a float x inside T's checked range or NaN,
+// T of 8-32 bits (the 64-bit targets select on f32_trunc_mag in get1/put1)
+template <typename T>
+__device__ __forceinline__ T f32_cast(float x) {
+    const uint32_t b = bits_to<uint32_t>(x);
+    const bool nan = f32_isnan(b);
+    const float xs = nan ? 0.0f : x;     // a C cast of NaN is undefined; of xs it is v_cvt_*_f32
+    if constexpr (std::is_same<T, int8_t>::value || std::is_same<T, uint8_t>::value ||
+                  std::is_same<T, int16_t>::value || std::is_same<T, uint16_t>::value) {
+        // through cvtt_i32: NaN -> INT32_MIN, whose low 8/16 bits are 0
+        return (T)(int32_t)xs;
+    } else if constexpr (std::is_same<T, int32_t>::value) {
+        return nan ? INT32_MIN : (int32_t)xs;
+    } else {
+        static_assert(std::is_same<T, uint32_t>::value, "64-bit targets: get1/put1 on the bits");
+        return nan ? 0u : (uint32_t)xs;                        // through cvtt_i64: low half of INT64_MIN
+    }
+}
+
+// d > hi || d < lo of GETF_CheckBND / NCX_PUT1F with d = (double)x, tested on
+// the float: an upper bound that is not a float (2^31-1, 2^32-1) rounds up
+// to the next power of two, and x > bound <=> x >= that power
+template <long long LO, unsigned long long HI>
+__device__ __forceinline__ bool f32_out_of_range(float x) {
+    constexpr double hi = (double)HI, lo = (double)LO;
+    constexpr float hf = (float)hi, lf = (float)lo;
+    static_assert((double)lf == lo, "every lower bound (0, -2^7, -2^15, -2^31, -2^63) is a float");
+    static_assert((double)hf >= hi, "an inexact upper bound rounds up to a power of two");
+    return ((double)hf == hi ? x > hf : x >= hf) || x < lf;
+}
+
 template <typename T>
 __device__ __forceinline__ double as_double(T v) {
     if constexpr (std::is_same<T, float>::value) return f32_to_f64(v);
@@ -189,6 +244,39 @@ __device__ __forceinline__ typename I<IT>::T get1(typename X<XT>::T xx, bool &ba
                 return II::fill();
             }
             return f64_to_f32(xx);
+        }
+    } else if constexpr (XT == NC_FLOAT) {
+        // float -> integer without the double (f32_cast above), written as
+        // selects (early returns became exec-mask branches: ~110 SALU per
+        // wave); the same rules: GETF_CheckBND2 for (u)longlong (:518-527),
+        // GETF_CheckBND + :511 for long, GETF_CheckBND (:503-513) otherwise
+        const uint32_t b = bits_to<uint32_t>(xx);
+        const uint32_t a = b & 0x7fffffffu;
+        const bool nan = f32_isnan(b), neg = (b >> 31) != 0;
+        if constexpr (IT == PNCX_ITYPE_LONGLONG || IT == PNCX_ITYPE_LONG) {
+            // |x| > 2^63 (not NaN): fill; +-2^63 exactly: INT64_MAX / INT64_MIN;
+            // NaN: cvttsd2si's INT64_MIN
+            const bool o = !nan && a > 0x5f000000u;
+            const uint64_t mag = f32_trunc_mag(b);
+            int64_t r = neg ? -(int64_t)mag : (int64_t)mag;
+            r = a == 0x5f000000u ? (neg ? INT64_MIN : INT64_MAX) : r;
+            r = nan ? INT64_MIN : r;
+            bad |= o;
+            return o ? II::fill() : r;
+        } else if constexpr (IT == PNCX_ITYPE_ULONGLONG) {
+            // x > 2^64 or x < 0 (not -0, not NaN): fill; 2^64 exactly:
+            // UINT64_MAX; NaN: 2^63 (cvtt_u64)
+            const bool o = !nan && (a > 0x5f800000u || (neg && a != 0));
+            uint64_t r = f32_trunc_mag(b);
+            r = a == 0x5f800000u ? UINT64_MAX : r;
+            r = nan ? 0x8000000000000000ull : r;
+            bad |= o;
+            return o ? II::fill() : r;
+        } else {
+            const bool o = f32_out_of_range<II::lo, II::hi>(xx);
+            const IT_T r = f32_cast<IT_T>(xx);
+            bad |= o;
+            return o ? II::fill() : r;
         }
     } else {
         const double d = as_double(xx);
@@ -231,8 +319,32 @@ __device__ __forceinline__ typename X<XT>::T put1(typename I<IT>::T v, typename 
         if (in_range(v, XI::lo, XI::hi)) return (XT_T)v;
         bad = true;
         return fill;
+    } else if constexpr (!XI::is_float && IT == PNCX_ITYPE_FLOAT) {
+        // NCX_PUT1F (:604-625) / NCX_PUTN_BYTE from float, on the float
+        // (f32_cast above), as selects; hi is 2^63 / 2^64 for the 64-bit
+        // externals
+        const bool o = f32_out_of_range<XI::lo, XI::hi>(v);
+        XT_T r;
+        if constexpr (XT == NC_INT64 || XT == NC_UINT64) {
+            const uint32_t b = bits_to<uint32_t>(v);
+            const uint32_t a = b & 0x7fffffffu;
+            const uint64_t mag = f32_trunc_mag(b);
+            if constexpr (XT == NC_INT64) {
+                // 2^63 (either sign) and NaN: cvttsd2si's INT64_MIN
+                const int64_t sv = (b >> 31) ? -(int64_t)mag : (int64_t)mag;
+                r = a >= 0x5f000000u ? INT64_MIN : sv;
+            } else {
+                // cvtt_u64: 2^64 -> 0, NaN -> 2^63, [0, 2^64) exact
+                uint64_t u = a == 0x5f800000u ? 0ull : mag;
+                r = f32_isnan(b) ? 0x8000000000000000ull : u;
+            }
+        } else {
+            r = f32_cast<XT_T>(v);
+        }
+        bad |= o;
+        return o ? fill : r;
     } else if constexpr (!XI::is_float && II::is_float) {
-        // NCX_PUT1F (:604-625) / NCX_PUTN_BYTE with a float itype
+        // NCX_PUT1F (:604-625) / NCX_PUTN_BYTE with a double itype
         const double d = as_double(v);
         const double hi = (double)XI::hi;     // 2^63 / 2^64 for the 64-bit ones
         const double lo = (double)XI::lo;

@@ -90,6 +90,11 @@ int pncx_device_count(void) { return pncxrt_device_count(); }
 int pncx_set_device(int dev) { return pncxrt_set_device(dev); }
 int pncx_get_device(void) { return pncxrt_get_device(); }
 
+int pncx_is_device_ptr(const void *p)
+{
+    return p != NULL && pncxrt_is_device_ptr(p);
+}
+
 int pncx_host_register(void *buf, pncx_offset nbytes)
 {
     if (buf == NULL || nbytes <= 0) return NC_EINVAL;

@@ -7,12 +7,15 @@
 // global_load_dwordx4 / global_store_dwordx4 on its own 16-byte-aligned
 // slice, so a wave moves 1 KiB per instruction, fully coalesced; UNROLL steps
 // are loaded before any is stored to keep several KiB in flight per wave.
-// The kernel is HBM-bound (no contraction: no MFMA, no LDS).
+// The kernels are HBM-bound (no contraction: no MFMA).  LDS stages the
+// narrow side of 4:1 / 8:1 widening and of narrowing tiles (Shape below).
 //
-// Status: a lane accumulates "some element was out of range"; at the end the
-// wave ballots it and one lane stores NC_ERANGE into *status.  This is the
-// reference's "return the first error" (ncx.m4:2487-2488) since NC_ERANGE is
-// the only error a conversion loop can produce.
+// Status: a lane accumulates "some element was out of range"; at the end
+// each wave ballots it and its first out-of-range lane stores the launch's
+// epoch into the block's flag word (Sink, publish); a second kernel reduces
+// the flags into the status word(s).  This is the reference's "return the
+// first error" (ncx.m4:2487-2488), since NC_ERANGE is the only error a
+// conversion loop can produce.
 #pragma once
 
 #include "pncx_device.hpp"
@@ -225,8 +228,17 @@ struct Sink {
 // the logical (XCD-remapped) block whose segment k_flags_batch looks up
 __device__ __forceinline__ void publish(const Sink &s, int *status, bool bad, int64_t fidx = -1) {
     if (s.flags != nullptr) {
-        // every thread of the block reaches this (kernels publish at the end)
-        if (__syncthreads_or(bad) && threadIdx.x == 0) s.flags[fidx < 0 ? (int64_t)blockIdx.x : fidx] = s.epoch;
+        // Per wave, no block barrier: the first out-of-range lane of each
+        // wave stores the epoch (waves of one block store the same value
+        // into the same word).  Round 2 reduced with __syncthreads_or, which
+        // compiles to a three-barrier LDS reduction every wave of a block
+        // waits in at its end; on a one-shot grid that tail was 2.8 LDS, ~30
+        // SALU and ~25 VALU instructions per wave (profiles/r03a_pmc_pairs.txt:
+        // byte -> uchar 78 % of peak against 84.6 % for byte -> schar, which
+        // publishes nothing).
+        const unsigned long long m = __ballot(bad);
+        if (m != 0 && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)m) - 1))
+            s.flags[fidx < 0 ? (int64_t)blockIdx.x : fidx] = s.epoch;
     } else {
         publish_status(status, bad, s.sval);
     }

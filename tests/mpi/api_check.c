@@ -5,20 +5,37 @@
  * test_gpu_c_api.py and tests/test_c_api_cpu.py run the modes and check
  * the files they write against the CPU oracle.
  *
- *   api_check c1 <nc> <in.bin> <n>
+ *   api_check c1 <nc> <in.bin> <n> [dev]
  *       BASELINE config 1 (benchmarks/C pattern, 1 rank): 1-D NC_INT x(n),
  *       ncmpi_put_vara_int_all of in.bin, close, reopen,
  *       ncmpi_get_vara_int_all (must equal the input) and
  *       ncmpi_get_vara_double_all (config 3's read: must equal (double)).
+ *       dev = 1: the user buffers are hipMalloc'ed (device-resident path).
+ *   api_check c1bench <nc> <n> <reps> <dev>
+ *       config 1 timed: reps x ncmpi_put_vara_int_all, then reps x
+ *       ncmpi_get_vara_int_all of 1-D NC_INT x(n) on one open file (host or
+ *       hipMalloc'ed buffers); prints median/min ms and the variable's offset.
+ *   api_check numrecs <nc>
+ *       on N ranks: collective record puts must leave numrecs in the FILE
+ *       (ncmpio_getput.m4:272-311), fixed-size puts must not touch it; rank
+ *       0 reads the header's numrecs bytes after every put.
+ *   api_check openfail <dir>
+ *       on 2+ ranks: with a file open, an open and a create that fail on
+ *       the last rank only must leave the open file usable everywhere, and
+ *       the failed create must remove its file.
+ *   api_check bputshort <nc>
+ *       bput_vara with a predefined buftype and a bufcount short of the
+ *       request: NC_EIOMISMATCH (ncmpio_i_getput.m4:216).
  *   api_check putvara <nc> <nvars> <len> <ntimes> <nonblocking> [indep]
  *       benchmarks/C/pnetcdf_put_vara.c:138-219 on 1..N ranks: record
  *       variables float var_i(time, Y, X), text/float/short attributes,
  *       ncmpi_iput_vara_float x nvars x ntimes + ncmpi_wait_all (or
  *       ncmpi_put_vara_float[_all]); each rank a 2-D block.
- *   api_check c4 <nc> <shorts.bin> <floats.bin> <nel> <erange>
+ *   api_check c4 <nc> <shorts.bin> <floats.bin> <nel> <erange> [dev]
  *       BASELINE config 4: 256 variables, ncmpi_iput_vara_short/float x 256
  *       + one ncmpi_wait_all; erange = 1 is §8(d)'s secondary variant (the
- *       NC_SHORT variables written from float with NC_ERANGE).
+ *       NC_SHORT variables written from float with NC_ERANGE).  dev = 1:
+ *       the 256 user buffers are hipMalloc'ed.
  *   api_check records <nc> <nrec> <x>
  *       config 5 at file level on N ranks: a record variable
  *       v(time, x) NC_DOUBLE, rank r writes its slab of records with
@@ -30,6 +47,7 @@
  *       define-mode only (dims, variables, text attributes) on N ranks: the
  *       header rank 0 writes must not depend on N.
  */
+#include <hip/hip_runtime_api.h>
 #include <mpi.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -62,28 +80,54 @@ static void *slurp(const char *path, size_t *len)
     return b;
 }
 
-static int mode_c1(const char *path, const char *inpath, MPI_Offset n)
+/* device copies of host data (hipMalloc), for the device-resident variants */
+static void *to_dev(const void *h, size_t n)
+{
+    void *d = NULL;
+    if (hipMalloc(&d, n ? n : 1) != hipSuccess) { fprintf(stderr, "hipMalloc failed\n"); exit(3); }
+    if (n && h && hipMemcpy(d, h, n, hipMemcpyHostToDevice) != hipSuccess) { fprintf(stderr, "H2D failed\n"); exit(3); }
+    return d;
+}
+static void from_dev(void *h, const void *d, size_t n)
+{
+    if (hipMemcpy(h, d, n, hipMemcpyDeviceToHost) != hipSuccess) { fprintf(stderr, "D2H failed\n"); exit(3); }
+}
+
+static int mode_c1(const char *path, const char *inpath, MPI_Offset n, int dev)
 {
     size_t len;
     int *in = (int *)slurp(inpath, &len), *got, ncid, dimid, varid, i;
     double *gd;
+    void *din = NULL, *dgot = NULL, *dgd = NULL;
     MPI_Offset start[1] = {0}, count[1] = {n}, put = 0, get = 0;
     if (in == NULL || len != (size_t)n * 4) { fprintf(stderr, "bad input\n"); return 1; }
+    got = (int *)calloc((size_t)n, sizeof(int));
+    gd = (double *)calloc((size_t)n, sizeof(double));
+    if (dev) {
+        din = to_dev(in, (size_t)n * 4);
+        dgot = to_dev(NULL, (size_t)n * 4);
+        dgd = to_dev(NULL, (size_t)n * 8);
+    }
     CHECK(ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid));
     CHECK(ncmpi_def_dim(ncid, "x", n, &dimid));
     CHECK(ncmpi_def_var(ncid, "v", NC_INT, 1, &dimid, &varid));
     CHECK(ncmpi_enddef(ncid));
-    CHECK(ncmpi_put_vara_int_all(ncid, varid, start, count, in));
+    CHECK(ncmpi_put_vara_int_all(ncid, varid, start, count, dev ? din : (void *)in));
     CHECK(ncmpi_inq_put_size(ncid, &put));
     CHECK(ncmpi_close(ncid));
-    got = (int *)calloc((size_t)n, sizeof(int));
-    gd = (double *)calloc((size_t)n, sizeof(double));
     CHECK(ncmpi_open(MPI_COMM_WORLD, path, NC_NOWRITE, MPI_INFO_NULL, &ncid));
     CHECK(ncmpi_inq_varid(ncid, "v", &varid));
-    CHECK(ncmpi_get_vara_int_all(ncid, varid, start, count, got));
-    CHECK(ncmpi_get_vara_double_all(ncid, varid, start, count, gd));
+    CHECK(ncmpi_get_vara_int_all(ncid, varid, start, count, dev ? dgot : (void *)got));
+    CHECK(ncmpi_get_vara_double_all(ncid, varid, start, count, dev ? dgd : (void *)gd));
     CHECK(ncmpi_inq_get_size(ncid, &get));
     CHECK(ncmpi_close(ncid));
+    if (dev) {
+        from_dev(got, dgot, (size_t)n * 4);
+        from_dev(gd, dgd, (size_t)n * 8);
+        hipFree(din);
+        hipFree(dgot);
+        hipFree(dgd);
+    }
     for (i = 0; i < n; i++) {
         if (got[i] != in[i]) { fprintf(stderr, "int mismatch at %d\n", i); nerrs++; break; }
         if (gd[i] != (double)in[i]) { fprintf(stderr, "double mismatch at %d\n", i); nerrs++; break; }
@@ -169,17 +213,23 @@ static int mode_putvara(const char *path, int nvars, int len, int ntimes, int no
     return nerrs != 0;
 }
 
-static int mode_c4(const char *path, const char *sp, const char *fp, MPI_Offset nel, int erange)
+static int mode_c4(const char *path, const char *sp, const char *fp, MPI_Offset nel, int erange, int dev)
 {
     const int nvar = 256;
     size_t ls, lf;
-    short *sh = (short *)slurp(sp, &ls);
-    float *fl = (float *)slurp(fp, &lf);
+    short *sh = (short *)slurp(sp, &ls), *hsh = NULL;
+    float *fl = (float *)slurp(fp, &lf), *hfl = NULL;
     int ncid, dimid, v, varid[256], reqs[256], st[256], err;
     MPI_Offset start[1] = {0}, count[1] = {nel};
     if (sh == NULL || fl == NULL || ls != (size_t)(nvar / 2) * nel * 2 || lf != (size_t)(nvar / 2) * nel * 4) {
         fprintf(stderr, "bad input\n");
         return 1;
+    }
+    if (dev) {                 /* the user buffers in HBM */
+        hsh = sh;
+        hfl = fl;
+        sh = (short *)to_dev(hsh, ls);
+        fl = (float *)to_dev(hfl, lf);
     }
     CHECK(ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid));
     CHECK(ncmpi_def_dim(ncid, "x", nel, &dimid));
@@ -199,6 +249,12 @@ static int mode_c4(const char *path, const char *sp, const char *fp, MPI_Offset 
     printf("{\"mode\": \"c4\", \"wait\": %d, \"statuses\": [", err);
     for (v = 0; v < nvar; v++) printf("%s%d", v ? ", " : "", st[v]);
     printf("], \"reqs_after\": %d, \"errors\": %d}\n", reqs[0], nerrs);
+    if (dev) {
+        hipFree(sh);
+        hipFree(fl);
+        sh = hsh;
+        fl = hfl;
+    }
     free(sh);
     free(fl);
     return nerrs != 0;
@@ -250,6 +306,164 @@ static int mode_records(const char *path, MPI_Offset nrec, MPI_Offset x)
     if (rank == 0) printf("{\"mode\": \"records\", \"nprocs\": %d, \"nrec\": %lld, \"errors\": %d}\n", nprocs,
                           (long long)nrec, nerrs);
     free(b);
+    return nerrs != 0;
+}
+
+static int cmp_dbl(const void *a, const void *b)
+{
+    const double x = *(const double *)a, y = *(const double *)b;
+    return x < y ? -1 : x > y;
+}
+
+/* config 1 timed (bench.py's c1 leg): one open file, reps puts then reps gets */
+static int mode_c1bench(const char *path, MPI_Offset n, int reps, int dev)
+{
+    int *h = (int *)malloc((size_t)n * 4), *g = (int *)calloc((size_t)n, 4), ncid, dimid, varid, r, bad = 0;
+    double *tp = (double *)calloc((size_t)reps, sizeof(double)), *tg = (double *)calloc((size_t)reps, sizeof(double));
+    void *dh = NULL, *dg = NULL;
+    MPI_Offset start[1] = {0}, count[1] = {n}, off = 0, i;
+    for (i = 0; i < n; i++) h[i] = (int)((uint32_t)i * 2654435761u);
+    if (dev) {
+        dh = to_dev(h, (size_t)n * 4);
+        dg = to_dev(NULL, (size_t)n * 4);
+    }
+    CHECK(ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid));
+    CHECK(ncmpi_def_dim(ncid, "x", n, &dimid));
+    CHECK(ncmpi_def_var(ncid, "v", NC_INT, 1, &dimid, &varid));
+    CHECK(ncmpi_enddef(ncid));
+    CHECK(ncmpi_inq_varoffset(ncid, varid, &off));
+    for (r = 0; r < reps; r++) {
+        const double t0 = MPI_Wtime();
+        CHECK(ncmpi_put_vara_int_all(ncid, varid, start, count, dev ? dh : (void *)h));
+        tp[r] = MPI_Wtime() - t0;
+    }
+    for (r = 0; r < reps; r++) {
+        const double t0 = MPI_Wtime();
+        CHECK(ncmpi_get_vara_int_all(ncid, varid, start, count, dev ? dg : (void *)g));
+        tg[r] = MPI_Wtime() - t0;
+    }
+    CHECK(ncmpi_close(ncid));
+    if (dev) from_dev(g, dg, (size_t)n * 4);
+    for (i = 0; i < n && !bad; i++) bad = g[i] != h[i];
+    if (bad) { fprintf(stderr, "c1bench: get differs from put\n"); nerrs++; }
+    qsort(tp, (size_t)reps, sizeof(double), cmp_dbl);
+    qsort(tg, (size_t)reps, sizeof(double), cmp_dbl);
+    printf("{\"mode\": \"c1bench\", \"n\": %lld, \"reps\": %d, \"dev\": %d, \"var_offset\": %lld, "
+           "\"put_ms_median\": %.5f, \"put_ms_min\": %.5f, \"get_ms_median\": %.5f, \"get_ms_min\": %.5f, "
+           "\"errors\": %d}\n", (long long)n, reps, dev, (long long)off, 1e3 * tp[reps / 2], 1e3 * tp[0],
+           1e3 * tg[reps / 2], 1e3 * tg[0], nerrs);
+    if (dev) { hipFree(dh); hipFree(dg); }
+    free(h); free(g); free(tp); free(tg);
+    return nerrs != 0;
+}
+
+/* numrecs as the FILE holds it (big-endian at byte 4; 8 bytes for CDF-5) */
+static long long file_numrecs(const char *path)
+{
+    unsigned char b[8];
+    long long v = 0;
+    int i;
+    FILE *f = fopen(path, "rb");
+    if (f == NULL || fseek(f, 4, SEEK_SET) != 0 || fread(b, 1, 8, f) != 8) { if (f) fclose(f); return -1; }
+    fclose(f);
+    for (i = 0; i < 8; i++) v = (v << 8) | b[i];
+    return v;
+}
+
+static int mode_numrecs(const char *path)
+{
+    int rank, nprocs, ncid, dimid[2], vr, vf, k;
+    long long seen[3];
+    int buf[16];
+    MPI_Offset start[2], count[2];
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    MPI_Comm_size(MPI_COMM_WORLD, &nprocs);
+    for (k = 0; k < 16; k++) buf[k] = rank * 100 + k;
+    CHECK(ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid));
+    CHECK(ncmpi_def_dim(ncid, "time", NC_UNLIMITED, &dimid[0]));
+    CHECK(ncmpi_def_dim(ncid, "x", 16, &dimid[1]));
+    CHECK(ncmpi_def_var(ncid, "r", NC_INT, 2, dimid, &vr));
+    CHECK(ncmpi_def_var(ncid, "f", NC_INT, 1, &dimid[1], &vf));
+    CHECK(ncmpi_enddef(ncid));
+    /* put 1: rank r writes record r */
+    start[0] = rank; start[1] = 0; count[0] = 1; count[1] = 16;
+    CHECK(ncmpi_put_vara_int_all(ncid, vr, start, count, buf));
+    MPI_Barrier(MPI_COMM_WORLD);
+    seen[0] = file_numrecs(path);
+    /* a fixed-size variable: numrecs unchanged */
+    start[0] = 0; count[0] = 16;
+    CHECK(ncmpi_put_vara_int_all(ncid, vf, start, count, buf));
+    MPI_Barrier(MPI_COMM_WORLD);
+    seen[1] = file_numrecs(path);
+    /* put 2: only rank 0 writes, record nprocs + 1 (others zero-length) */
+    start[0] = nprocs + 1; start[1] = 0; count[0] = rank == 0 ? 1 : 0; count[1] = 16;
+    CHECK(ncmpi_put_vara_int_all(ncid, vr, start, count, buf));
+    MPI_Barrier(MPI_COMM_WORLD);
+    seen[2] = file_numrecs(path);
+    CHECK(ncmpi_close(ncid));
+    MPI_Allreduce(MPI_IN_PLACE, &nerrs, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);
+    if (rank == 0)
+        printf("{\"mode\": \"numrecs\", \"nprocs\": %d, \"after_rec_put\": %lld, \"after_fix_put\": %lld, "
+               "\"after_second_rec_put\": %lld, \"at_close\": %lld, \"errors\": %d}\n", nprocs, seen[0], seen[1],
+               seen[2], file_numrecs(path), nerrs);
+    return nerrs != 0;
+}
+
+static int mode_openfail(const char *dir)
+{
+    char a[512], b[512], c[512];
+    int rank, nprocs, ncid, dimid, varid, id2 = -7, e_open, e_create, got[8], i, vals[8];
+    MPI_Offset start[1] = {0}, count[1] = {8};
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    MPI_Comm_size(MPI_COMM_WORLD, &nprocs);
+    for (i = 0; i < 8; i++) vals[i] = 10 * rank + i;
+    snprintf(a, sizeof a, "%s/a.nc", dir);
+    snprintf(c, sizeof c, "%s/c.nc", dir);
+    /* the last rank names a file that does not exist / a directory that does not */
+    if (rank == nprocs - 1) snprintf(b, sizeof b, "%s/missing.nc", dir);
+    else snprintf(b, sizeof b, "%s/a.nc", dir);
+    CHECK(ncmpi_create(MPI_COMM_WORLD, a, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid));
+    CHECK(ncmpi_def_dim(ncid, "x", 8 * nprocs, &dimid));
+    CHECK(ncmpi_def_var(ncid, "v", NC_INT, 1, &dimid, &varid));
+    CHECK(ncmpi_enddef(ncid));
+    e_open = ncmpi_open(MPI_COMM_WORLD, b, NC_NOWRITE, MPI_INFO_NULL, &id2);
+    if (rank == nprocs - 1) snprintf(c, sizeof c, "%s/nodir/c.nc", dir);
+    e_create = ncmpi_create(MPI_COMM_WORLD, c, NC_CLOBBER, MPI_INFO_NULL, &id2);
+    /* the first file is still open and usable on every rank */
+    start[0] = 8 * rank;
+    CHECK(ncmpi_put_vara_int_all(ncid, varid, start, count, vals));
+    CHECK(ncmpi_get_vara_int_all(ncid, varid, start, count, got));
+    for (i = 0; i < 8; i++)
+        if (got[i] != vals[i]) { fprintf(stderr, "rank %d: a.nc data lost\n", rank); nerrs++; break; }
+    CHECK(ncmpi_close(ncid));
+    MPI_Allreduce(MPI_IN_PLACE, &nerrs, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);
+    if (rank == 0) {
+        FILE *f;
+        snprintf(c, sizeof c, "%s/c.nc", dir);
+        f = fopen(c, "rb");
+        printf("{\"mode\": \"openfail\", \"nprocs\": %d, \"open\": %d, \"create\": %d, \"c_exists\": %d, "
+               "\"errors\": %d}\n", nprocs, e_open, e_create, f != NULL, nerrs);
+        if (f) fclose(f);
+    }
+    return nerrs != 0;
+}
+
+static int mode_bputshort(const char *path)
+{
+    int ncid, dimid, varid, req = -5, vals[16] = {0}, e_short, e_ok, st = -1;
+    MPI_Offset start[1] = {0}, count[1] = {16};
+    CHECK(ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid));
+    CHECK(ncmpi_def_dim(ncid, "x", 16, &dimid));
+    CHECK(ncmpi_def_var(ncid, "v", NC_INT, 1, &dimid, &varid));
+    CHECK(ncmpi_enddef(ncid));
+    CHECK(ncmpi_buffer_attach(ncid, 1024));
+    e_short = ncmpi_bput_vara(ncid, varid, start, count, vals, 8, MPI_INT, &req);
+    e_ok = ncmpi_bput_vara(ncid, varid, start, count, vals, 16, MPI_INT, &req);
+    CHECK(ncmpi_wait_all(ncid, 1, &req, &st));
+    CHECK(ncmpi_buffer_detach(ncid));
+    CHECK(ncmpi_close(ncid));
+    printf("{\"mode\": \"bputshort\", \"short\": %d, \"exact\": %d, \"status\": %d, \"errors\": %d}\n", e_short, e_ok,
+           st, nerrs);
     return nerrs != 0;
 }
 
@@ -367,11 +581,18 @@ int main(int argc, char **argv)
 {
     int rc = 2;
     MPI_Init(&argc, &argv);
-    if (argc >= 5 && strcmp(argv[1], "c1") == 0) rc = mode_c1(argv[2], argv[3], atoll(argv[4]));
+    if (argc >= 5 && strcmp(argv[1], "c1") == 0)
+        rc = mode_c1(argv[2], argv[3], atoll(argv[4]), argc >= 6 ? atoi(argv[5]) : 0);
+    else if (argc >= 6 && strcmp(argv[1], "c1bench") == 0)
+        rc = mode_c1bench(argv[2], atoll(argv[3]), atoi(argv[4]), atoi(argv[5]));
+    else if (argc >= 3 && strcmp(argv[1], "numrecs") == 0) rc = mode_numrecs(argv[2]);
+    else if (argc >= 3 && strcmp(argv[1], "openfail") == 0) rc = mode_openfail(argv[2]);
+    else if (argc >= 3 && strcmp(argv[1], "bputshort") == 0) rc = mode_bputshort(argv[2]);
     else if (argc >= 7 && strcmp(argv[1], "putvara") == 0)
         rc = mode_putvara(argv[2], atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), atoi(argv[6]),
                           argc >= 8 ? atoi(argv[7]) : 0);
-    else if (argc >= 7 && strcmp(argv[1], "c4") == 0) rc = mode_c4(argv[2], argv[3], argv[4], atoll(argv[5]), atoi(argv[6]));
+    else if (argc >= 7 && strcmp(argv[1], "c4") == 0)
+        rc = mode_c4(argv[2], argv[3], argv[4], atoll(argv[5]), atoi(argv[6]), argc >= 8 ? atoi(argv[7]) : 0);
     else if (argc >= 5 && strcmp(argv[1], "records") == 0) rc = mode_records(argv[2], atoll(argv[3]), atoll(argv[4]));
     else if (argc >= 3 && strcmp(argv[1], "errors") == 0) rc = mode_errors(argv[2]);
     else if (argc >= 3 && strcmp(argv[1], "header") == 0) rc = mode_header(argv[2]);

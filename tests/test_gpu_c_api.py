@@ -123,15 +123,19 @@ def _var_bytes(raw, h, name, rec=None):
     return raw[off:off + per * T.xlen(v["xtype"])]
 
 
-def test_config1_put_get_vara_int_all(gpu, tmp_path):
+@pytest.mark.parametrize("dev", [0, 1], ids=["host", "device"])
+def test_config1_put_get_vara_int_all(gpu, tmp_path, dev):
     """BASELINE config 1 through the public API: 2^20 NC_INT
-    put_vara_int_all, then get_vara_int_all and get_vara_double_all."""
+    put_vara_int_all, then get_vara_int_all and get_vara_double_all (config
+    3's read).  dev = 1: the user buffers are hipMalloc'ed, so the same
+    ncmpi_* calls take the device-resident path (converted in HBM, the
+    external bytes across PCIe once)."""
     n = 1 << 20
     v = np.random.default_rng(0x5EED0001).integers(-2**31, 2**31 - 1, n, dtype=np.int64).astype(np.int32)
     v[:4] = [-2**31, 2**31 - 1, 0, -1]
     inp, nc = str(tmp_path / "in.bin"), str(tmp_path / "c1.nc")
     v.tofile(inp)
-    out = _json(capi.run([capi.exe("api_check"), "c1", nc, inp, str(n)]))
+    out = _json(capi.run([capi.exe("api_check"), "c1", nc, inp, str(n), str(dev)]))
     assert out["errors"] == 0 and out["put_size"] == 4 * n and out["get_size"] == 8 * n
     raw = open(nc, "rb").read()
     h = cdfparse.parse_cdf(raw)
@@ -181,11 +185,14 @@ def test_put_vara_benchmark_pattern_ranks(gpu, tmp_path, nprocs):
     _check_putvara(nc, out, 3, 48, 2)
 
 
+@pytest.mark.parametrize("dev", [0, 1], ids=["host", "device"])
 @pytest.mark.parametrize("erange", [0, 1])
-def test_config4_iput_batch(gpu, tmp_path, erange):
+def test_config4_iput_batch(gpu, tmp_path, erange, dev):
     """BASELINE config 4 through the public API: 256 iput_vara_short/float
     + one wait_all (one batched conversion); erange = 1: the NC_SHORT
-    variables from float in [-40000, 40000] (SURVEY §8(d) secondary)."""
+    variables from float in [-40000, 40000] (SURVEY §8(d) secondary).
+    dev = 1: the 256 user buffers are hipMalloc'ed; the wait converts them
+    with pncx_dev_batch in HBM."""
     nel = 1 << 16
     rng = np.random.default_rng(0x5EED0004)
     sh = rng.integers(-32768, 32767, 128 * nel, dtype=np.int16)
@@ -193,7 +200,7 @@ def test_config4_iput_batch(gpu, tmp_path, erange):
     sp, fp, nc = str(tmp_path / "s.bin"), str(tmp_path / "f.bin"), str(tmp_path / "c4.nc")
     sh.tofile(sp)
     fl.tofile(fp)
-    out = _json(capi.run([capi.exe("api_check"), "c4", nc, sp, fp, str(nel), str(erange)]))
+    out = _json(capi.run([capi.exe("api_check"), "c4", nc, sp, fp, str(nel), str(erange), str(dev)]))
     assert out["errors"] == 0 and out["reqs_after"] == -1          # NC_REQ_NULL after the wait
     ora = OracleConv()
     raw = open(nc, "rb").read()
@@ -248,3 +255,52 @@ def test_reference_benchmark_runs_on_libpnetcdf(gpu, tmp_path, args):
     r = capi.run([REF_BENCH, "-k", "5", "-l", "32", "-n", "3", "-t", "2"] + args + [nc])
     assert "Write bandwidth" in r.stdout
     _check_putvara(nc, {"py": 1, "px": 1, "nprocs": 1}, 3, 32, 2)
+
+
+@pytest.mark.parametrize("dev", [0, 1], ids=["host", "device"])
+def test_config1_bench_mode(gpu, tmp_path, dev):
+    """bench.py's c1 leg: repeated put_vara_int_all / get_vara_int_all on
+    one open file, host or hipMalloc'ed buffers; the last get must equal
+    the put and the file must hold the oracle's bytes."""
+    n = 1 << 16
+    nc = str(tmp_path / "c1b.nc")
+    out = _json(capi.run([capi.exe("api_check"), "c1bench", nc, str(n), "3", str(dev)]))
+    assert out["errors"] == 0 and out["put_ms_median"] > 0 and out["get_ms_median"] > 0
+    vals = (np.arange(n, dtype=np.uint64) * 2654435761 % (1 << 32)).astype(np.uint32).view(np.int32)
+    exp, st = OracleConv().putn(5, T.NC_INT, vals, T.ITYPE_INT, T.fill_bytes(T.NC_INT))
+    raw = open(nc, "rb").read()
+    assert st == 0 and raw[out["var_offset"]:out["var_offset"] + 4 * n] == exp
+
+
+@pytest.mark.parametrize("nprocs", [1, 2])
+def test_numrecs_written_by_collective_record_puts(gpu, tmp_path, nprocs):
+    """ncmpio_getput.m4:272-311: a collective put of a record variable
+    writes the MAX record count into the file at once; a fixed-size put
+    leaves it alone.  Rank 0 reads the header bytes between the puts."""
+    if nprocs > 1 and not capi.have_mpiexec():
+        pytest.skip("mpiexec not available")
+    nc = str(tmp_path / "nr.nc")
+    out = _json(capi.run([capi.exe("api_check"), "numrecs", nc], nprocs=nprocs))
+    assert out["errors"] == 0
+    assert out["after_rec_put"] == nprocs
+    assert out["after_fix_put"] == nprocs
+    assert out["after_second_rec_put"] == nprocs + 2
+    assert out["at_close"] == nprocs + 2
+
+
+@pytest.mark.skipif(not capi.have_mpiexec(), reason="mpiexec not available")
+def test_failed_open_and_create_keep_other_file(gpu, tmp_path):
+    """an open or create that fails on one rank only fails on
+    every rank, must not close the file the ranks already have open (it is
+    pncx_nc id 0 on every rank), and a failed create removes its file."""
+    out = _json(capi.run([capi.exe("api_check"), "openfail", str(tmp_path)], nprocs=2))
+    assert out["errors"] == 0
+    assert out["open"] < 0                 # NC_ENOENT on the last rank, the MIN on every rank
+    assert out["create"] < 0 and out["c_exists"] == 0
+
+
+def test_bput_short_bufcount(gpu, tmp_path):
+    """bput_vara with a predefined buftype and bufcount short of
+    the request is NC_EIOMISMATCH, not a read past the buffer."""
+    out = _json(capi.run([capi.exe("api_check"), "bputshort", str(tmp_path / "b.nc")]))
+    assert out["errors"] == 0 and out["short"] == T.NC_EIOMISMATCH and out["exact"] == 0 and out["status"] == 0

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 31)
     ap.add_argument("--all", action="store_true")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--pairs", default="", help="comma list of dir:xtype:itype, e.g. get:float:ulonglong")
     args = ap.parse_args()
     import torch
     from pnetcdf_amd import nctypes as T
@@ -30,7 +31,12 @@ def main():
     st = torch.zeros(1, dtype=torch.int32, device="cuda")
     sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     px, pi, ps = (ctypes.c_void_p(t.data_ptr()) for t in (xbuf, ibuf, st))
-    if args.all:
+    if args.pairs:
+        pairs = []
+        for tok in args.pairs.split(","):
+            d, x, i = tok.split(":")
+            pairs.append((T.PNCX_GET if d == "get" else T.PNCX_PUT, T.XTYPES[x], T.ITYPES[i]))
+    elif args.all:
         pairs = [(d, x, i) for d in (T.PNCX_GET, T.PNCX_PUT) for x in T.NUMERIC_XTYPES for i in T.NUMERIC_ITYPES]
     else:
         pairs = [(T.PNCX_GET, T.NC_INT, T.ITYPE_DOUBLE), (T.PNCX_GET, T.NC_DOUBLE, T.ITYPE_DOUBLE),
