@@ -308,6 +308,7 @@ class Workload:
 class C2Swap(Workload):
     def __init__(self, torch, lib, sptr, slab_gib, world, rank):
         from pnetcdf_amd.shard import record_slab
+        self.check_desc = ""
         n = int(slab_gib * GIB) // 8                           # NC_DOUBLE elements per rank
         rec_elems = 8192 * 16384                               # one 1 GiB record of v(time, 8192, 16384)
         nrec_total = (n // rec_elems) * world
@@ -325,6 +326,8 @@ class C2Swap(Workload):
         self._torch, self._n = torch, n
         self.elems, self.bytes_per_elem, self.slab_per_elem = n, 16, 8
         self.metric_key, self.dtype = "swap8", "u64"
+        self.check_desc = ("every element of the slab against the splitmix64 values regenerated on the GPU, "
+                           "byte-reversed by torch when the pass count is odd")
         self.kernel = "k_tile<SwapOp<8>, true>"
         self.cfg = {"workload": ("C2: 32 GiB contiguous NC_DOUBLE get_vara, in-place 8-byte swap" if world == 1 else
                                  f"C5: NC_DOUBLE record variable v(time={nrec_total}, 8192, 16384), "
@@ -368,6 +371,7 @@ class C3IntDouble(Workload):
         self.launch = lambda: _ok(lib.pncx_dev_getn(5, T.NC_INT, px, pi, n, T.ITYPE_DOUBLE, ps, sptr))
         self.elems, self.bytes_per_elem, self.slab_per_elem = n, 12, 4
         self.metric_key, self.dtype = "get_int_double", "int32->f64"
+        self.check_desc = "every element against torch's byte flip + int32->double cast of the input; status NC_NOERR"
         self.kernel = "k_tile<GetOp<NC_INT, double>, true>"
         self.cfg = {"workload": "C3: NC_INT on disk read via get_vara_double, fused 4-byte swap + int32->double",
                     "elements_per_gpu": n, "xtype": "NC_INT", "itype": "double"}
@@ -433,6 +437,8 @@ class C4Batch(Workload):
         self.bytes_per_elem = per_pair / 2.0
         self.slab_per_elem = 3
         self.metric_key = "batch_c4_erange" if self._erange else "batch_c4"
+        self.check_desc = ("all 256 statuses and every output element against torch's byte flip (same-type) or "
+                           "trunc + NC_SHORT fill outside [-32768, 32767] (float -> NC_SHORT)")
         self.dtype = "f32->i16/f32" if self._erange else "i16/f32"
         self.kernel = ("k_batch<PutOp<NC_SHORT, float>> + k_batch_swapmix" if self._erange
                        else "k_batch_swapmix")
@@ -529,6 +535,7 @@ def measure(torch, lib, group, stream, wl, steps, warmup):
         lib.pncx_dev_batch_timing(0)
     else:
         kern_ms = sum(a.elapsed_time(b) for a, b in evs) / steps
+    wl.rank_kernel_ms = kern_ms
     elapsed, kern_ms = group.max([elapsed, kern_ms])
     return elapsed, kern_ms, call_ms
 
@@ -544,6 +551,94 @@ def summary(wl, elapsed, kern_ms, call_ms, steps, world):
     if call_ms is not None:
         roof["call_ms_avg"] = round(call_ms, 4)
     return value, elapsed * 1e3 / steps, roof
+
+
+def c1_leg(reps=21, n=1 << 20):
+    """BASELINE configs[0]: 1-D 2^20 NC_INT ncmpi_put_vara_int_all +
+    ncmpi_get_vara_int_all through libpnetcdf.so (tests/mpi/api_check
+    c1bench, one MPI rank, a file on tmpfs /dev/shm), with host buffers
+    (8 I/O threads, and 1 to match the reference's single writer) and with
+    hipMalloc'ed buffers.  Rates are external (file) bytes / call time."""
+    exe = os.path.join(ROOT, "tests", "mpi", "api_check")
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
+    path = os.path.join(shm, f"pncx_c1_{os.getpid()}.nc")
+    res = {}
+    xbytes = 4.0 * n
+    for key, dev, threads in (("host_8_io_threads", 0, None), ("host_1_io_thread", 0, "1"), ("device_buffers", 1, None)):
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if threads is not None:
+            env["PNCX_IO_THREADS"] = threads
+        r = subprocess.run([exe, "c1bench", path, str(n), str(reps), str(dev)], capture_output=True, text=True,
+                           timeout=300, env=env)
+        if r.returncode != 0:
+            res[key] = {"error": r.returncode, "stderr": r.stderr[-400:]}
+            continue
+        o = json.loads(r.stdout.strip().splitlines()[-1])
+        res[key] = {"put_ms": o["put_ms_median"], "get_ms": o["get_ms_median"],
+                    "put_GiBps": round(xbytes / (o["put_ms_median"] * 1e-3) / GIB, 3),
+                    "get_GiBps": round(xbytes / (o["get_ms_median"] * 1e-3) / GIB, 3), "errors": o["errors"]}
+        res["var_offset"] = o["var_offset"]
+    return res, path
+
+
+def c1_reference_sequence(path, var_offset, reps=21, n=1 << 20):
+    """The reference's C1 sequence restated with the oracle on one host
+    thread (cpu_baseline of the c1 leg): put = swap the user buffer in place,
+    pwrite, swap it back (ncmpio_getput.m4:186-214,269-270); get = pread +
+    in-place swap (ncmpio_getput.m4:422-470 -> ncmpio_unpack_xbuf)."""
+    from oracle import oracle as O
+    lib = O.lib()
+    h = (np.arange(n, dtype=np.uint64) * 2654435761 % (1 << 32)).astype(np.uint32)
+    g = np.empty(n, np.uint32)
+    fd = os.open(path, os.O_RDWR)
+    tp, tg = [], []
+    try:
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            lib.orc_in_swapn(h.ctypes.data_as(ctypes.c_void_p), n, 4)
+            os.pwrite(fd, h.data, var_offset)
+            lib.orc_in_swapn(h.ctypes.data_as(ctypes.c_void_p), n, 4)
+            tp.append(time.perf_counter() - t0)
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            os.preadv(fd, [g.data], var_offset)
+            lib.orc_in_swapn(g.ctypes.data_as(ctypes.c_void_p), n, 4)
+            tg.append(time.perf_counter() - t0)
+    finally:
+        os.close(fd)
+    ok = bool(np.array_equal(g, h))
+    put_ms, get_ms = 1e3 * sorted(tp)[reps // 2], 1e3 * sorted(tg)[reps // 2]
+    xbytes = 4.0 * n
+    return {"value": round(2 * xbytes / ((put_ms + get_ms) * 1e-3) / GIB, 3), "unit": "GiB/s", "cores": 1,
+            "kind": "port", "put_ms": round(put_ms, 4), "get_ms": round(get_ms, 4), "check_ok": ok,
+            "sample": f"the whole C1 request ({n} NC_INT, 4 MiB) on the same tmpfs file, median of {reps}: "
+                      f"orc_in_swapn + pwrite + orc_in_swapn back / pread + orc_in_swapn, 1 thread"}
+
+
+def c1_workload(cpu=True):
+    res, path = c1_leg()
+    out = {"unit": "GiB/s", "config": {
+        "workload": "C1: benchmarks/C pattern, 1 MPI rank on tmpfs: 1-D 2^20 NC_INT ncmpi_put_vara_int_all + "
+                    "ncmpi_get_vara_int_all through libpnetcdf.so",
+        "elements": 1 << 20, "xtype": "NC_INT", "itype": "int", "file": "/dev/shm"},
+        "note": "value = external bytes of one put + one get / (put_ms + get_ms), host buffers, 8 I/O threads; "
+                "host-memory boundary: PCIe-bound, not an HBM roofline case (roofline null)",
+        "roofline": None, "legs": res}
+    h = res.get("host_8_io_threads", {})
+    ok = all(isinstance(v, dict) and v.get("errors", 1) == 0 for k, v in res.items() if k != "var_offset")
+    if "put_ms" in h:
+        out["value"] = round(2 * 4.0 * (1 << 20) / ((h["put_ms"] + h["get_ms"]) * 1e-3) / GIB, 3)
+        out["ms_per_step"] = round(h["put_ms"] + h["get_ms"], 4)
+    if cpu and "var_offset" in res:
+        out["cpu_baseline"] = c1_reference_sequence(path, res["var_offset"])
+        ok = ok and out["cpu_baseline"]["check_ok"]
+    out["check_ok"] = ok
+    try:
+        os.unlink(path)
+    except OSError:
+        pass
+    return out
 
 
 def add_cpu_baselines(wls, budget):
@@ -574,6 +669,16 @@ def add_cpu_baselines(wls, budget):
         del jobs, keep
 
 
+def device_identity(torch, local):
+    """PCI domain:bus:device of this rank's GPU as one number (a float64
+    holds it exactly), for the distinct-device check at N > 1."""
+    p = torch.cuda.get_device_properties(local)
+    dom, bus, dev = (int(getattr(p, k, -1)) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    if bus < 0:
+        return float(local), f"local{local}"
+    return float((dom << 16) | (bus << 8) | dev), f"{dom:04x}:{bus:02x}:{dev:02x}"
+
+
 def worker(args):
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -600,6 +705,25 @@ def worker(args):
     group = Group(dist, torch.device("cuda", local) if backend == "nccl" else "cpu")
     stream = torch.cuda.current_stream()
     sptr = ctypes.c_void_p(stream.cuda_stream)
+    ranks = None
+    if world > 1:
+        # one process per GPU: every rank's GPU must be a different device
+        # (PCI address gathered over the group); the gloo rehearsal puts
+        # every rank on GPU 0 on purpose and says so
+        ident, name = device_identity(torch, local)
+        ids = [r[0] for r in group.all_gather_floats([ident])]
+        distinct = len(set(ids)) == world
+        ranks = {"backend": "rccl" if backend == "nccl" else backend, "world_size": world,
+                 "local_device_of_rank0": name, "distinct_devices": distinct,
+                 "pci_of_ranks": ["%04x:%02x:%02x" % ((int(i) >> 16), (int(i) >> 8) & 0xFF, int(i) & 0xFF)
+                                  for i in ids]}
+        if backend == "nccl":
+            ranks["rccl_world_size"] = dist.get_world_size()
+            if not distinct:
+                if rank == 0:
+                    print(f"bench.py: ranks share GPUs {ranks['pci_of_ranks']}; refusing to report a "
+                          f"{world}-GPU number", file=sys.stderr)
+                return 2
 
     # ------------------------------------------------ headline (value)
     head = "c4" if args.workload == "c4_async" else args.workload
@@ -607,8 +731,10 @@ def worker(args):
         args.async_batch = True
     wl = make_workload(args.workload if args.workload != "c4_async" else "c4", torch, lib, sptr, args, world, rank)
     elapsed, kern_ms, call_ms = measure(torch, lib, group, stream, wl, args.steps, args.warmup)
-    ok = wl.check()
+    ok = group.all_true(wl.check())
     value, ms_per_step, roof = summary(wl, elapsed, kern_ms, call_ms, args.steps, world)
+    if ranks is not None:
+        ranks["kernel_ms_per_rank"] = [round(r[0], 4) for r in group.all_gather_floats([wl.rank_kernel_ms])]
     gather = None
     if world > 1 and args.gather_gib > 0 and head == "c2":
         gib = args.gather_gib if backend == "nccl" else min(args.gather_gib, 1.0)   # gloo rehearsal: 1 GiB
@@ -630,6 +756,7 @@ def worker(args):
         "config": wl.cfg,
         "roofline": roof,
         "check_ok": ok,
+        "check": wl.check_desc + (" (on every rank, AND-reduced)" if world > 1 else ""),
     }
     wl.free()
     del wl
@@ -644,10 +771,12 @@ def worker(args):
             v, mps, rf = summary(w, el, km, cm, args.extra_steps, world)
             extra[name] = {"value": round(v, 2), "unit": "GiB/s", "ms_per_step": round(mps, 4),
                            "steps": args.extra_steps, "dtype": w.dtype, "config": w.cfg, "roofline": rf,
-                           "check_ok": w.check()}
+                           "check_ok": w.check(), "check": w.check_desc}
             w.free()
             del w
             torch.cuda.empty_cache()
+        if not args.no_c1:
+            extra["c1"] = c1_workload(cpu=rank == 0 and not args.no_cpu_baseline)
         line["workloads"] = extra
 
     if rank == 0:
@@ -660,6 +789,8 @@ def worker(args):
             line["cpu_baseline"] = None
         if gather is not None:
             line["gather"] = gather
+        if ranks is not None:
+            line["ranks"] = ranks
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
@@ -675,7 +806,8 @@ def main(argv=None):
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c4_async", "c4_erange"])
     ap.add_argument("--slab-gib", type=float, default=32.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="N=1, c2: skip the c3/c4 workloads")
+    ap.add_argument("--no-extra", action="store_true", help="N=1, c2: skip the c3/c4/c1 workloads")
+    ap.add_argument("--no-c1", action="store_true", help="N=1, c2: skip the c1 file-level leg")
     ap.add_argument("--extra-steps", type=int, default=200,
                     help="timed calls of each extra workload (20 calls of ~0.25 ms read 2-5 %% high: the rate settles "
                          "over the first ~100, profiles/r02s_bench_x200.json)")

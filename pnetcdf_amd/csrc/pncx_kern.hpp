@@ -2,11 +2,9 @@
 //
 // One kernel template serves every conversion class.  An "Op" says how one
 // source element (raw bits as loaded) becomes one destination element (raw
-// bits as stored) and how many elements a lane handles per step (VEC, chosen
-// so the narrower side moves exactly 16 bytes).  Per step a lane issues
-// global_load_dwordx4 / global_store_dwordx4 on its own 16-byte-aligned
-// slice, so a wave moves 1 KiB per instruction, fully coalesced; UNROLL steps
-// are loaded before any is stored to keep several KiB in flight per wave.
+// bits as stored).  k_tile gives each 256-lane block one tile (a one-shot
+// grid; lanes loop only past 2^23 blocks) shaped by Shape<Op>: every global
+// load and store instruction of a wave covers one contiguous 1 KiB.
 // The kernels are HBM-bound (no contraction: no MFMA).  LDS stages the
 // narrow side of 4:1 / 8:1 widening and of narrowing tiles (Shape below).
 //

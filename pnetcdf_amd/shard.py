@@ -93,6 +93,21 @@ class Group:
         self.dist.all_gather(out, t)
         return [int(x.item()) for x in out]
 
+    def all_gather_floats(self, values):
+        """Every rank's list of floats (equal lengths), on every rank:
+        [[rank 0's values], [rank 1's], ...]."""
+        if self.dist is None:
+            return [list(values)]
+        import torch
+        t = torch.tensor(list(values), dtype=torch.float64, device=self.device)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [[float(v) for v in o.cpu()] for o in out]
+
+    def all_true(self, flag):
+        """True on every rank iff flag holds on every rank."""
+        return self.max([0.0 if flag else 1.0])[0] == 0.0
+
     def first_error(self, status):
         """min over ranks of an NC status (0 = NC_NOERR, negatives = errors)."""
         if self.dist is None:

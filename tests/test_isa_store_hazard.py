@@ -1,0 +1,172 @@
+"""The store-data hazard, checked on the shipped ISA (CPU).
+
+On gfx940+ a VALU write to the VGPRs holding the data of a vector-memory
+store of more than 64 bits needs 2 wait states after the store (LLVM's
+GCNHazardRecognizer inserts them for the stores it emits).  The streaming
+store `st_stream` (pnetcdf_amd/csrc/pncx_kern.hpp) is inline asm the
+compiler cannot see into, so it carries its own `s_nop 1`; round 2 shipped
+a kernel without it that corrupted 8 of 16 bytes.  This test disassembles
+every gfx950 code object inside libpncx.so (the clang offload bundles of the
+.hip_fatbin section) and checks EVERY global/buffer store of 96 or 128 data
+bits, compiler-emitted or asm: within the 2 wait states after it (s_nop N
+counts N+1, any other instruction 1) no VALU instruction may write one of
+its data VGPRs, on the fall-through path or at a branch target reached
+before the window closes.
+"""
+import os
+import re
+import struct
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "pnetcdf_amd", "lib", "libpncx.so")
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+STORE = re.compile(r"^\s*(global|buffer|flat)_store_dwordx([34])\s+(.*?)\s*//")
+VREG = re.compile(r"v\[(\d+):(\d+)\]|\bv(\d+)\b")
+
+
+def code_objects(path):
+    """The gfx950 ELF code objects of every offload bundle in the library."""
+    data = open(path, "rb").read()
+    out, pos = [], 0
+    while True:
+        i = data.find(MAGIC, pos)
+        if i < 0:
+            return out
+        (cnt,) = struct.unpack_from("<Q", data, i + 24)
+        p = i + 32
+        for _ in range(cnt):
+            off, size, tl = struct.unpack_from("<QQQ", data, p)
+            p += 24
+            triple = data[p:p + tl].decode()
+            p += tl
+            if "gfx950" in triple and size:
+                out.append(data[i + off:i + off + size])
+        pos = i + 1
+
+
+def regs(operand):
+    m = VREG.search(operand)
+    if m is None:
+        return set()
+    if m.group(1) is not None:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    return {int(m.group(3))}
+
+
+def data_regs(mnem, ops):
+    """The data VGPRs of a store: global/flat `vaddr, vdata, ...`; buffer `vdata, vaddr, ...`."""
+    parts = [x.strip() for x in ops.split(",")]
+    return regs(parts[0] if mnem == "buffer" else parts[1])
+
+
+ADDR = re.compile(r"//\s*([0-9A-Fa-f]+):")
+
+
+def _addr(line):
+    m = ADDR.search(line)
+    return int(m.group(1), 16) if m else None
+
+
+def _branch_target(s, addr):
+    """target address of s_branch / s_cbranch_* (simm16 in dwords after pc+4)"""
+    imm = int(s.split()[1].split("/")[0].strip(), 0)
+    if imm >= 1 << 15:
+        imm -= 1 << 16
+    return addr + 4 + 4 * imm
+
+
+def _walk(lines, at, k, dregs, waits, depth, bad, store):
+    """Scan from line index k with `waits` wait states done; follow both
+    edges of conditional branches until 2 wait states are covered."""
+    while k < len(lines) and waits < 2:
+        s = lines[k].strip()
+        k += 1
+        if not s or s.startswith("<") or s.endswith(":") or ADDR.search(s) is None:
+            continue
+        ins = s.split()[0]
+        if ins == "s_nop":
+            waits += int(s.split()[1].split("/")[0].strip(), 0) + 1
+        elif ins.startswith(("s_endpgm", "s_setpc", "s_swappc")):
+            return
+        elif ins.startswith(("s_branch", "s_cbranch")):
+            if depth > 4:
+                bad.append(("branch chain too deep", store, s))
+                return
+            tgt = at.get(_branch_target(s, _addr(s)))
+            if tgt is None:
+                bad.append(("branch target not found", store, s))
+                return
+            _walk(lines, at, tgt, dregs, waits + 1, depth + 1, bad, store)
+            if ins.startswith("s_branch"):
+                return
+            waits += 1
+        else:
+            if ins.startswith("v_") and not ins.startswith(("v_readlane", "v_readfirstlane", "v_cmp_", "v_cmpx_")):
+                dst = s[len(ins):].split("//")[0].split(",")[0]
+                if regs(dst) & dregs:
+                    bad.append(("VALU writes store data", store, s))
+                    return
+            waits += 1
+        if waits >= 2:
+            return
+
+
+def check(lines):
+    """(stores checked, violations) over one disassembly."""
+    at = {}
+    for k, line in enumerate(lines):
+        a = _addr(line)
+        if a is not None:
+            at[a] = k
+    n, bad = 0, []
+    for k, line in enumerate(lines):
+        m = STORE.match(line)
+        if m is None:
+            continue
+        n += 1
+        _walk(lines, at, k + 1, data_regs(m.group(1), m.group(3)), 0, 0, bad, line.strip())
+    return n, bad
+
+
+@pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(OBJDUMP)), reason="library or llvm-objdump missing")
+def test_wide_stores_have_two_wait_states(tmp_path):
+    cos = code_objects(LIB)
+    assert len(cos) >= 4, "expected one gfx950 code object per kernel TU"
+    total, asm_stores, violations = 0, 0, []
+    for j, co in enumerate(cos):
+        p = tmp_path / f"co{j}.elf"
+        p.write_bytes(co)
+        dis = subprocess.run([OBJDUMP, "-d", "--mcpu=gfx950", str(p)], capture_output=True, text=True,
+                             check=True).stdout.splitlines()
+        n, bad = check(dis)
+        total += n
+        asm_stores += sum(1 for x in dis if STORE.match(x) and " nt sc1" in x)
+        violations += bad
+    assert asm_stores > 100, asm_stores         # the streaming stores are there and were checked
+    assert not violations, violations[:5]
+    assert total >= asm_stores
+
+
+def test_checker_catches_the_round2_bug():
+    """The checker itself: the round-2 sequence (asm store, then a VALU
+    reusing its data registers at once) is flagged; with s_nop 1 it is not."""
+    buggy = ["\tglobal_store_dwordx4 v[6:7], v[0:3], off nt sc1 // 000000000000: DE7E8000 007F0006",
+             "\tv_mov_b32_e32 v1, 0 // 000000000008: 7E020280"]
+    fixed = [buggy[0], "\ts_nop 1 // 000000000008: BF800001", "\tv_mov_b32_e32 v1, 0 // 00000000000C: 7E020280"]
+    one = [buggy[0], "\tv_mov_b32_e32 v9, 0 // 000000000008: 7E120280",
+           "\tv_mov_b32_e32 v1, 0 // 00000000000C: 7E020280"]                   # 1 wait state: still a hazard
+    two = [buggy[0], "\tv_mov_b32_e32 v9, 0 // 000000000008: 7E120280",
+           "\ts_add_u32 s2, s2, s4 // 00000000000C: 80020402",
+           "\tv_mov_b32_e32 v1, 0 // 000000000010: 7E020280"]
+    assert check(buggy)[1] and check(one)[1] and not check(fixed)[1] and not check(two)[1]
+    # a branch straight back to a VALU that overwrites the data: flagged through the target
+    loop = ["\tv_mov_b32_e32 v2, 0 // 000000000000: 7E040280",
+            "\tglobal_store_dwordx4 v[6:7], v[0:3], off // 000000000004: DC7C8000 007F0006",
+            "\ts_cbranch_vccz 65532 // 00000000000C: BF86FFFC",
+            "\ts_endpgm // 000000000010: BF810000"]
+    assert check(loop)[1]
