@@ -365,9 +365,26 @@ struct Shape {
     static constexpr int W = SS > DS ? SS : DS, N = SS < DS ? SS : DS, R = W / N;
     // narrowing 2:1 also stages (16 B stores per lane instead of 8 B)
     static constexpr bool USE_LDS = R >= 4 || (R == 2 && SS > DS);
+    static constexpr int LANES = 256;
+    // Occupancy of the 4:1 and 8:1 tiles (either direction) is capped with
+    // LDS the block does not use: the rate of a streaming tile depends on the
+    // bytes the CU keeps in flight, best near 64-80 KiB.  A 256-lane 8:1
+    // tile moves 36 KiB, so 2 blocks per CU; a 4:1 tile 20 KiB, 4 blocks;
+    // an uncapped CU holds 8 blocks (tools/widen_sweep.hip occupancy
+    // sweep, profiles/r03_occupancy_sweep_b.txt, same box: NC_BYTE ->
+    // double 73.1 % at 8 blocks per CU, 79.9 % at 2; NC_SHORT -> double
+    // 76.5 / 81.8 % at 8 / 4; float -> NC_BYTE 79.7 / 82.7 %; double ->
+    // NC_BYTE 80.9 / 85.3 % at 8 / 2; while a 1:1 swap (8 KiB per tile)
+    // falls from 84.7 % to 75.7 % at 4).  The LDS is handed out in two
+    // 80 KiB halves per CU (27 KiB gave 6 blocks, 32 and 40 KiB 4, 54 and
+    // 80 KiB 2), so 48 KiB gives 2 blocks per CU and 40 KiB gives 4.
+    static constexpr int OCC_LDS = R >= 8 ? 48 * 1024 : R == 4 ? 40 * 1024 : 0;
     static constexpr int E = USE_LDS ? 16 / N : 16 / W;  // elements per lane per tile
-    static constexpr int TILE = 256 * E;                  // elements per block tile
+    static constexpr int TILE = LANES * E;                // elements per block tile
     static constexpr int E2 = 16 / W;                     // elements per wide 16 B chunk
+    static constexpr int LDS_BYTES = USE_LDS ? 16 * LANES : 16;
+    // dynamic LDS requested at launch on top of the static tile
+    static constexpr int PAD_LDS = OCC_LDS > LDS_BYTES ? OCC_LDS - LDS_BYTES : 0;
 };
 
 template <int B> struct VecT;
@@ -408,7 +425,7 @@ template <class Op, bool NT>
 __device__ __forceinline__ void tile_body(const uint8_t *src, uint8_t *dst, typename Op::fill_t fill,
                                           bool &bad, uint8_t *lds) {
     using S = Shape<Op>;
-    constexpr int SS = S::SS, DS = S::DS;
+    constexpr int SS = S::SS, DS = S::DS, L = S::LANES;
     const int lane = threadIdx.x;
     if constexpr (!S::USE_LDS) {
         constexpr int E = S::E, SB = E * SS, DB = E * DS;
@@ -433,10 +450,10 @@ __device__ __forceinline__ void tile_body(const uint8_t *src, uint8_t *dst, type
         // times in a row)
         NV w[R];
 #pragma unroll
-        for (int k = 0; k < R; k++) w[k] = *reinterpret_cast<const NV *>(lds + (k * 256 + lane) * E2 * SS);
+        for (int k = 0; k < R; k++) w[k] = *reinterpret_cast<const NV *>(lds + (k * L + lane) * E2 * SS);
 #pragma unroll
         for (int k = 0; k < R; k++) {
-            const int c = k * 256 + lane;                      // wide chunk index
+            const int c = k * L + lane;                        // wide chunk index
             alignas(16) uint8_t sb[E2 * SS];
             alignas(16) uint8_t db[16];
             __builtin_memcpy(sb, &w[k], E2 * SS);
@@ -450,7 +467,7 @@ __device__ __forceinline__ void tile_body(const uint8_t *src, uint8_t *dst, type
         constexpr int R = S::R, E2 = S::E2;
 #pragma unroll
         for (int k = 0; k < R; k++) {
-            const int c = k * 256 + lane;
+            const int c = k * L + lane;
             alignas(16) uint8_t sb[16];
             alignas(16) uint8_t db[E2 * DS];
             const auto w = ldv<16, NT>(src + c * 16);
@@ -465,24 +482,24 @@ __device__ __forceinline__ void tile_body(const uint8_t *src, uint8_t *dst, type
     }
 }
 
-// scalar remainder [e0, n) by the 256 threads of one block
-template <class Op>
+// scalar remainder [e0, n) by the L threads of one block
+template <class Op, int L = 256>
 __device__ __forceinline__ void scalar_range(const uint8_t *src, uint8_t *dst, int64_t e0, int64_t n,
                                              typename Op::fill_t fill, bool &bad) {
-    for (int64_t e = e0 + threadIdx.x; e < n; e += 256) scalar_elem<Op>(src, dst, e, fill, bad);
+    for (int64_t e = e0 + threadIdx.x; e < n; e += L) scalar_elem<Op>(src, dst, e, fill, bad);
 }
 
 template <class Op, bool NT>
-__global__ __launch_bounds__(256) void k_tile(const uint8_t *src, uint8_t *dst, int64_t head,
-                                              int64_t ntile, int64_t n, typename Op::fill_t fill,
-                                              Sink sk) {
+__global__ __launch_bounds__(Shape<Op>::LANES) void k_tile(const uint8_t *src, uint8_t *dst, int64_t head,
+                                                           int64_t ntile, int64_t n, typename Op::fill_t fill,
+                                                           Sink sk) {
     using S = Shape<Op>;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[S::USE_LDS ? 4096 : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[S::LDS_BYTES];
     bool bad = false;
     const int64_t nb = gridDim.x;
     if (blockIdx.x == 0) {                               // scalar head and remainder
-        for (int64_t e = threadIdx.x; e < head; e += 256) scalar_elem<Op>(src, dst, e, fill, bad);
-        scalar_range<Op>(src, dst, head + ntile * S::TILE, n, fill, bad);
+        scalar_range<Op, S::LANES>(src, dst, 0, head, fill, bad);
+        scalar_range<Op, S::LANES>(src, dst, head + ntile * S::TILE, n, fill, bad);
     }
     const uint8_t *ts = src + head * S::SS;
     uint8_t *td = dst + head * S::DS;
@@ -517,10 +534,10 @@ __global__ __launch_bounds__(256) void k_scalar(const uint8_t *src, uint8_t *dst
 constexpr int BATCH_STEPS = 1;  // tiles per block
 
 template <class Op, bool NT>
-__global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg, const int *map,
-                                               pncxk_groups grp, Sink sk) {
+__global__ __launch_bounds__(Shape<Op>::LANES) void k_batch(const pncxk_seg *segs, int nseg, const int *map,
+                                                            pncxk_groups grp, Sink sk) {
     using S = Shape<Op>;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[S::USE_LDS ? 4096 : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[S::LDS_BYTES];
     const long long b = batch_block();   // logical block: segment lookup and flag slot
     const int lo = batch_segment<true>(b, map, grp, segs, nseg);
     const pncxk_seg sg = segs[lo];
@@ -531,8 +548,8 @@ __global__ __launch_bounds__(256) void k_batch(const pncxk_seg *segs, int nseg, 
     bool bad = false;
     const int64_t rel = b - sg.block0;
     if (rel == 0) {
-        for (int64_t e = threadIdx.x; e < sg.head; e += 256) scalar_elem<Op>(src, dst, e, fill, bad);
-        scalar_range<Op>(src, dst, sg.head + ntile * S::TILE, sg.n, fill, bad);
+        scalar_range<Op, S::LANES>(src, dst, 0, sg.head, fill, bad);
+        scalar_range<Op, S::LANES>(src, dst, sg.head + ntile * S::TILE, sg.n, fill, bad);
     }
     if (rel < ntile)
         tile_body<Op, NT>(src + (sg.head + rel * (int64_t)S::TILE) * S::SS,
@@ -1030,11 +1047,11 @@ int launch_stream(const pncxk_args *a) {
         if (grid > MAX_BLOCKS) grid = MAX_BLOCKS;
         sk = sink_acquire(a->status, NC_ERANGE, st, grid, want);
         if (a->nontemporal >= 0)
-            hipLaunchKernelGGL((k_tile<Op, true>), dim3((unsigned)grid), dim3(256), 0, st, src, dst, h,
-                               ntile, n, fill, sk);
+            hipLaunchKernelGGL((k_tile<Op, true>), dim3((unsigned)grid), dim3(Shape<Op>::LANES), Shape<Op>::PAD_LDS, st,
+                               src, dst, h, ntile, n, fill, sk);
         else
-            hipLaunchKernelGGL((k_tile<Op, false>), dim3((unsigned)grid), dim3(256), 0, st, src, dst, h,
-                               ntile, n, fill, sk);
+            hipLaunchKernelGGL((k_tile<Op, false>), dim3((unsigned)grid), dim3(Shape<Op>::LANES), Shape<Op>::PAD_LDS, st,
+                               src, dst, h, ntile, n, fill, sk);
     }
     return sink_finish(sk, st, grid, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
 }
@@ -1049,11 +1066,11 @@ int launch_batch(const pncxk_batch_args *a) {
     // reduce is not timed)
     hipEvent_t e0 = (hipEvent_t)a->ev_start, e1 = (hipEvent_t)a->ev_stop;
     if (e0 != nullptr || e1 != nullptr)
-        hipExtLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0, st, e0, e1, 0, a->dsegs,
-                              a->nseg, a->dmap, a->grp, sk);
+        hipExtLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(Shape<Op>::LANES),
+                              Shape<Op>::PAD_LDS, st, e0, e1, 0, a->dsegs, a->nseg, a->dmap, a->grp, sk);
     else
-        hipLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(256), 0, st, a->dsegs, a->nseg,
-                           a->dmap, a->grp, sk);
+        hipLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(Shape<Op>::LANES), Shape<Op>::PAD_LDS,
+                           st, a->dsegs, a->nseg, a->dmap, a->grp, sk);
     return sink_finish_batch(sk, a->dsegs, a->nseg, a->nblocks, st, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
 }
 

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--all", action="store_true")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--pairs", default="", help="comma list of dir:xtype:itype, e.g. get:float:ulonglong")
+    ap.add_argument("--no-status", action="store_true", help="pass no status word (no NC_ERANGE tracking)")
     args = ap.parse_args()
     import torch
     from pnetcdf_amd import nctypes as T
@@ -31,6 +32,8 @@ def main():
     st = torch.zeros(1, dtype=torch.int32, device="cuda")
     sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     px, pi, ps = (ctypes.c_void_p(t.data_ptr()) for t in (xbuf, ibuf, st))
+    if args.no_status:
+        ps = None
     if args.pairs:
         pairs = []
         for tok in args.pairs.split(","):

@@ -20,6 +20,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <functional>
 #include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
@@ -108,26 +109,93 @@ template <> struct NV<8> { typedef uint64_t t; };
 
 // ---- widening variants: narrow src (n elems), wide dst ---------------------
 // blk: 256-lane block = one tile of 256*16 narrow bytes
-template <class Op>
-__global__ __launch_bounds__(256) void w_blk(const uint8_t *src, uint8_t *dst, int64_t ntile) {
+template <class Op, int L = 256>
+__global__ __launch_bounds__(L) void w_blk(const uint8_t *src, uint8_t *dst, int64_t ntile) {
     constexpr int R = Op::WS / Op::NS, PB = 16 / R;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[4096];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[16 * L];
     const int64_t t = xcd(blockIdx.x, gridDim.x);
     if (t >= ntile) return;
     const int lane = threadIdx.x;
-    *reinterpret_cast<u32x4 *>(lds + lane * 16) = ld16(src + t * 4096 + lane * 16);
+    *reinterpret_cast<u32x4 *>(lds + lane * 16) = ld16(src + t * 16 * L + lane * 16);
     __syncthreads();
     typename NV<PB>::t w[R];
 #pragma unroll
-    for (int k = 0; k < R; k++) w[k] = *reinterpret_cast<const typename NV<PB>::t *>(lds + (k * 256 + lane) * PB);
+    for (int k = 0; k < R; k++) w[k] = *reinterpret_cast<const typename NV<PB>::t *>(lds + (k * L + lane) * PB);
 #pragma unroll
-    for (int k = 0; k < R; k++) st16(dst + (t * 256 * R + k * 256 + lane) * 16, widen16<Op>((const uint8_t *)&w[k]));
+    for (int k = 0; k < R; k++) st16(dst + (t * L * R + k * L + lane) * 16, widen16<Op>((const uint8_t *)&w[k]));
 }
+// blk with its LDS tile in dynamic shared memory, so the launch can ask for
+// more LDS than the tile needs and cap the blocks per CU (occupancy)
+template <class Op, int L>
+__global__ __launch_bounds__(L) void w_blkd(const uint8_t *src, uint8_t *dst, int64_t ntile) {
+    constexpr int R = Op::WS / Op::NS, PB = 16 / R;
+    extern __shared__ __attribute__((aligned(16))) uint8_t dlds[];
+    const int64_t t = xcd(blockIdx.x, gridDim.x);
+    if (t >= ntile) return;
+    const int lane = threadIdx.x;
+    *reinterpret_cast<u32x4 *>(dlds + lane * 16) = ld16(src + t * 16 * L + lane * 16);
+    __syncthreads();
+    typename NV<PB>::t w[R];
+#pragma unroll
+    for (int k = 0; k < R; k++) w[k] = *reinterpret_cast<const typename NV<PB>::t *>(dlds + (k * L + lane) * PB);
+#pragma unroll
+    for (int k = 0; k < R; k++) st16(dst + (t * L * R + k * L + lane) * 16, widen16<Op>((const uint8_t *)&w[k]));
+}
+template <class Op, int L>
+__global__ __launch_bounds__(L) void n_blkd(const uint8_t *src, uint8_t *dst, int64_t ntile, int *flags) {
+    constexpr int R = Op::WS / Op::NS, PB = 16 / R;
+    extern __shared__ __attribute__((aligned(16))) uint8_t dlds[];
+    const int64_t t = xcd(blockIdx.x, gridDim.x);
+    if (t >= ntile) return;
+    const int lane = threadIdx.x;
+    bool bad = false;
+    u32x4 v[R];
+#pragma unroll
+    for (int k = 0; k < R; k++) v[k] = ld16(src + (t * L * R + k * L + lane) * 16);
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+        uint8_t nb[PB];
+        narrow16<Op>(v[k], nb, bad);
+        typename NV<PB>::t x;
+        __builtin_memcpy(&x, nb, PB);
+        *reinterpret_cast<typename NV<PB>::t *>(dlds + (k * L + lane) * PB) = x;
+    }
+    __syncthreads();
+    st16(dst + t * 16 * L + lane * 16, *reinterpret_cast<const u32x4 *>(dlds + lane * 16));
+    const unsigned long long m = __ballot(bad);
+    if (m && (lane & 63) == (unsigned)(__ffsll((long long)m) - 1)) flags[blockIdx.x] = 1;
+}
+
+// 1:1 8-byte swap, 16 B per lane (C2's shape) and NC_INT -> double (C3's
+// direct shape: 8 B read, 16 B written per lane), LDS only as occupancy cap
+__global__ __launch_bounds__(256) void k_swap8d(const uint8_t *src, uint8_t *dst, int64_t ntile) {
+    extern __shared__ uint8_t dlds[];
+    const int64_t t = xcd(blockIdx.x, gridDim.x);
+    if (t >= ntile) return;
+    u32x4 v = ld16(src + (t * 256 + threadIdx.x) * 16);
+    u32x4 o = {__builtin_bswap32(v.y), __builtin_bswap32(v.x), __builtin_bswap32(v.w), __builtin_bswap32(v.z)};
+    if (v.x == 0x12345678u) dlds[threadIdx.x] = 1;
+    st16(dst + (t * 256 + threadIdx.x) * 16, o);
+}
+__global__ __launch_bounds__(256) void k_i2dd(const uint8_t *src, uint8_t *dst, int64_t ntile) {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    extern __shared__ uint8_t dlds[];
+    const int64_t t = xcd(blockIdx.x, gridDim.x);
+    if (t >= ntile) return;
+    const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(src + (t * 256 + threadIdx.x) * 8));
+    const double a = (double)(int32_t)__builtin_bswap32(v.x), b = (double)(int32_t)__builtin_bswap32(v.y);
+    u32x4 o;
+    __builtin_memcpy(&o, &a, 8);
+    __builtin_memcpy((uint8_t *)&o + 8, &b, 8);
+    if (v.x == 0x12345678u) dlds[threadIdx.x] = 1;
+    st16(dst + (t * 256 + threadIdx.x) * 16, o);
+}
+
 // wave: each wave its own 1 KiB of narrow bytes, no block barrier
 template <class Op, int TPW>
-__global__ __launch_bounds__(256) void w_wave(const uint8_t *src, uint8_t *dst, int64_t nwt) {
+__global__ __launch_bounds__(1024) void w_wave(const uint8_t *src, uint8_t *dst, int64_t nwt) {
     constexpr int R = Op::WS / Op::NS, PB = 16 / R;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[4096 * TPW];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[16384 * TPW];
     const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int64_t wt0 = (xcd(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + wv) * TPW;   // first wave tile
     uint8_t *my = lds + wv * 1024 * TPW;
@@ -149,8 +217,8 @@ __global__ __launch_bounds__(256) void w_wave(const uint8_t *src, uint8_t *dst, 
     }
 }
 // direct: R narrow loads of PB bytes per lane, R stores
-template <class Op>
-__global__ __launch_bounds__(256) void w_direct(const uint8_t *src, uint8_t *dst, int64_t ntile) {
+template <class Op, int L = 256>
+__global__ __launch_bounds__(L) void w_direct(const uint8_t *src, uint8_t *dst, int64_t ntile) {
     constexpr int R = Op::WS / Op::NS, PB = 16 / R;
     const int64_t t = xcd(blockIdx.x, gridDim.x);
     if (t >= ntile) return;
@@ -158,9 +226,9 @@ __global__ __launch_bounds__(256) void w_direct(const uint8_t *src, uint8_t *dst
     typename NV<PB>::t w[R];
 #pragma unroll
     for (int k = 0; k < R; k++)
-        w[k] = __builtin_nontemporal_load(reinterpret_cast<const typename NV<PB>::t *>(src + t * 4096 + (k * 256 + lane) * PB));
+        w[k] = __builtin_nontemporal_load(reinterpret_cast<const typename NV<PB>::t *>(src + t * 16 * L + (k * L + lane) * PB));
 #pragma unroll
-    for (int k = 0; k < R; k++) st16(dst + (t * 256 * R + k * 256 + lane) * 16, widen16<Op>((const uint8_t *)&w[k]));
+    for (int k = 0; k < R; k++) st16(dst + (t * L * R + k * L + lane) * 16, widen16<Op>((const uint8_t *)&w[k]));
 }
 
 // ---- narrowing variants: wide src, narrow dst ------------------------------
@@ -275,6 +343,9 @@ static void widen_case(const char *name, int64_t moved) {
         {"wave2", [&] { hipLaunchKernelGGL((w_wave<Op, 2>), dim3((nwt + 7) / 8), dim3(256), 0, 0, g_src, g_dst, nwt); }},
         {"wave64", [&] { hipLaunchKernelGGL((w_wave<Op, 1>), dim3(nwt), dim3(64), 0, 0, g_src, g_dst, nwt); }},
         {"direct", [&] { hipLaunchKernelGGL(w_direct<Op>, dim3(ntile), dim3(256), 0, 0, g_src, g_dst, ntile); }},
+        {"blk1024", [&] { hipLaunchKernelGGL((w_blk<Op, 1024>), dim3(ntile / 4), dim3(1024), 0, 0, g_src, g_dst, ntile / 4); }},
+        {"wave1024", [&] { hipLaunchKernelGGL((w_wave<Op, 1>), dim3(nwt / 16), dim3(1024), 0, 0, g_src, g_dst, nwt); }},
+        {"dir1024", [&] { hipLaunchKernelGGL((w_direct<Op, 1024>), dim3(ntile / 4), dim3(1024), 0, 0, g_src, g_dst, ntile / 4); }},
     };
     for (int rep = 0; rep < 2; rep++)
         for (auto &v : vs) {
@@ -324,6 +395,49 @@ static void narrow_case(const char *name, int64_t moved) {
         }
 }
 
+// occupancy: blocks of L lanes with `lds` bytes of LDS each (>= the tile)
+template <class Op, bool widen>
+static void occ_case(const char *name, int64_t moved) {
+    constexpr int R = Op::WS / Op::NS;
+    const int64_t nbytes_n = moved / (1 + R) / 16384 * 16384;
+    const double alg = (double)nbytes_n * (1 + R);
+    static const int cfg[][2] = {{256, 4096}, {256, 27306}, {256, 32768}, {256, 40960}, {256, 54613},
+                                 {256, 81920}, {1024, 16384}, {1024, 98304}};
+    for (auto &c : cfg) {
+        const int L = c[0], lds = c[1];
+        const int64_t ntile = nbytes_n / (16 * L);
+        std::function<void()> f;
+        if constexpr (widen) {
+            if (L == 256) f = [&, lds, ntile] { hipLaunchKernelGGL((w_blkd<Op, 256>), dim3(ntile), dim3(256), lds, 0, g_src, g_dst, ntile); };
+            else f = [&, lds, ntile] { hipLaunchKernelGGL((w_blkd<Op, 1024>), dim3(ntile), dim3(1024), lds, 0, g_src, g_dst, ntile); };
+        } else {
+            if (L == 256) f = [&, lds, ntile] { hipLaunchKernelGGL((n_blkd<Op, 256>), dim3(ntile), dim3(256), lds, 0, g_src, g_dst, ntile, g_flags); };
+            else f = [&, lds, ntile] { hipLaunchKernelGGL((n_blkd<Op, 1024>), dim3(ntile), dim3(1024), lds, 0, g_src, g_dst, ntile, g_flags); };
+        }
+        const int per_cu = std::min(163840 / lds, 2048 / L);
+        const float ms = time_it(f);
+        printf("%-22s lanes=%4d lds=%6d blocks/CU<=%2d waves/CU<=%2d %8.4f ms %5.1f %%\n", name, L, lds, per_cu,
+               per_cu * L / 64, ms, alg / ms / 1e6 / 80.0);
+    }
+}
+
+static void occ_direct(int64_t moved) {
+    static const int ldss[] = {0, 27306, 32768, 40960, 54613, 81920};
+    for (int which = 0; which < 2; which++)
+        for (int lds : ldss) {
+            const int bpl = which == 0 ? 32 : 24;                   // bytes moved per lane
+            const int64_t ntile = moved / (256 * (int64_t)bpl);
+            std::function<void()> f = which == 0
+                ? std::function<void()>([&, lds, ntile] { hipLaunchKernelGGL(k_swap8d, dim3(ntile), dim3(256), lds, 0, g_src, g_dst, ntile); })
+                : std::function<void()>([&, lds, ntile] { hipLaunchKernelGGL(k_i2dd, dim3(ntile), dim3(256), lds, 0, g_src, g_dst, ntile); });
+            const int per_cu = lds ? std::min(163840 / lds, 8) : 8;
+            const float ms = time_it(f);
+            const double alg = (double)ntile * 256 * bpl;
+            printf("%-22s lanes= 256 lds=%6d blocks/CU<=%2d waves/CU<=%2d %8.4f ms %5.1f %%\n",
+                   which == 0 ? "swap8 out-of-place" : "get int->double", lds, per_cu, per_cu * 4, ms, alg / ms / 1e6 / 80.0);
+        }
+}
+
 __global__ void k_fill(uint64_t *p, int64_t n, uint64_t seed) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         uint64_t z = seed + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ull;
@@ -350,11 +464,27 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&g_flags, 64 << 20));
     hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (uint64_t *)g_src, moved / 8, 0x5EEDull);
     CK(hipDeviceSynchronize());
+    if (argc > 2 && argv[2][0] == 'o') {
+        for (int r = 0; r < 2; r++) occ_direct(moved);
+        for (int r = 0; r < 2; r++) {
+            occ_case<B2D, true>("get byte->double", moved);
+            occ_case<S2D, true>("get short->double", moved);
+            occ_case<B2F, true>("get byte->float", moved);
+        }
+        hipLaunchKernelGGL(k_fill_f64, dim3(4096), dim3(256), 0, 0, (double *)g_src, moved / 8);
+        CK(hipDeviceSynchronize());
+        for (int r = 0; r < 2; r++) occ_case<D2B, false>("put double->byte", moved);
+        hipLaunchKernelGGL(k_fill_f32, dim3(4096), dim3(256), 0, 0, (float *)g_src, moved / 4);
+        CK(hipDeviceSynchronize());
+        for (int r = 0; r < 2; r++) occ_case<F2B, false>("put float->byte", moved);
+        return 0;
+    }
     widen_case<B2D>("get byte->double", moved);
     widen_case<S2D>("get short->double", moved);
     widen_case<B2F>("get byte->float", moved);
     hipLaunchKernelGGL(k_fill_f64, dim3(4096), dim3(256), 0, 0, (double *)g_src, moved / 8);
     CK(hipDeviceSynchronize());
+    if (argc > 2) return 0;
     narrow_case<D2B>("put double->byte", moved);
     hipLaunchKernelGGL(k_fill_f32, dim3(4096), dim3(256), 0, 0, (float *)g_src, moved / 4);
     CK(hipDeviceSynchronize());
