@@ -1402,6 +1402,17 @@ static void batch_time(ctx_t *c)
     c->tcpend++;
 }
 
+/* PNCX_BATCH_FUSE=0 launches every class of a batch on its own (A/B) */
+static int batch_fuse_enabled(void)
+{
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("PNCX_BATCH_FUSE");
+        v = e == NULL || atoi(e) != 0;
+    }
+    return v;
+}
+
 /* launch the class kernels of a plan whose descriptors are on the device */
 static int launch_classes(const cls_t *cls, int ncls, uint8_t *dbase, size_t soff, size_t moff, int sval,
                           int build_maps, void *stream, ctx_t *tc)
@@ -1420,6 +1431,38 @@ static int launch_classes(const cls_t *cls, int ncls, uint8_t *dbase, size_t sof
     if (tc != NULL) tc->tnext = tc->timing && !timed ? -1 : 0;
     pncxk_seg *dseg = (pncxk_seg *)(dbase + soff);
     int *dmap = (int *)(dbase + moff);
+    /* a conversion class beside the same-type swaps (C4's NC_ERANGE variant:
+     * float -> NC_SHORT + the NC_FLOAT swaps): one fused launch
+     * (k_batch_fused), one ramp and drain instead of two */
+    if (ncls == 2 && batch_fuse_enabled()) {
+        const int mi = cls[0].op.kind == PNCXK_SWAPMIX ? 0 : cls[1].op.kind == PNCXK_SWAPMIX ? 1 : -1;
+        const cls_t *cv = mi >= 0 ? &cls[1 - mi] : NULL, *mx = mi >= 0 ? &cls[mi] : NULL;
+        if (cv != NULL && (cv->op.kind == PNCXK_GET || cv->op.kind == PNCXK_PUT)) {
+            pncxk_batch_args ba[2];
+            const cls_t *cc[2] = {cv, mx};
+            int j, rc;
+            for (j = 0; j < 2; j++) {
+                ba[j].dsegs = dseg + cc[j]->first;
+                ba[j].nseg = cc[j]->count;
+                ba[j].nblocks = cc[j]->nblocks;
+                ba[j].dmap = cc[j]->map_off >= 0 ? dmap + cc[j]->map_off : NULL;
+                ba[j].grp = cc[j]->grp;
+                ba[j].sval = sval;
+                ba[j].stream = stream;
+                ba[j].ev_start = ba[j].ev_stop = NULL;
+                if (ba[j].dmap != NULL && build_maps && (err = pncxk_batch_map(&ba[j])) != 0) return err;
+            }
+            if (timed) {
+                ba[0].ev_start = tc->tev[2 * tc->tpend];
+                ba[0].ev_stop = tc->tev[2 * tc->tpend + 1];
+            }
+            rc = pncxk_batch_fused(cv->op.kind, cv->op.a, cv->op.b, cv->op.c, &ba[0], &ba[1]);
+            if (rc != PNCXK_NOFUSE) {
+                if (!rc && timed) tc->tnext = 1;
+                return rc;
+            }
+        }
+    }
     for (k = 0; k < ncls && !err; k++) {
         const cls_t *c = &cls[k];
         pncxk_batch_args ba;

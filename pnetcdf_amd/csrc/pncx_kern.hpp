@@ -420,14 +420,17 @@ __device__ __forceinline__ void conv_regs(const uint8_t *sb, uint8_t *db, typena
     __builtin_memcpy(db, d, sizeof d);
 }
 
-// one full tile: src/dst point at the tile's first element
+// one full tile: src/dst point at the tile's first element.  `lane` is the
+// thread's lane in the tile's LANES; with valid == false the thread moves no
+// data but still meets the tile's LDS barrier (the fused batch kernel runs
+// four tiles per block, the last of which may be absent).
 template <class Op, bool NT>
 __device__ __forceinline__ void tile_body(const uint8_t *src, uint8_t *dst, typename Op::fill_t fill,
-                                          bool &bad, uint8_t *lds) {
+                                          bool &bad, uint8_t *lds, const int lane, const bool valid) {
     using S = Shape<Op>;
     constexpr int SS = S::SS, DS = S::DS, L = S::LANES;
-    const int lane = threadIdx.x;
     if constexpr (!S::USE_LDS) {
+        if (!valid) return;
         constexpr int E = S::E, SB = E * SS, DB = E * DS;
         alignas(16) uint8_t sb[SB];
         alignas(16) uint8_t db[DB];
@@ -441,9 +444,12 @@ __device__ __forceinline__ void tile_body(const uint8_t *src, uint8_t *dst, type
         // widening: narrow src 16 B/lane -> LDS -> R wide 16 B chunks per lane
         constexpr int R = S::R, E2 = S::E2;
         using NV = typename VecT<E2 * SS>::type;
-        const auto v = ldv<16, NT>(src + lane * 16);
-        *reinterpret_cast<typename VecT<16>::type *>(lds + lane * 16) = v;
+        if (valid) {
+            const auto v = ldv<16, NT>(src + lane * 16);
+            *reinterpret_cast<typename VecT<16>::type *>(lds + lane * 16) = v;
+        }
         __syncthreads();
+        if (!valid) return;
         // all R LDS reads before the first store: the streaming store is an
         // asm statement with a memory clobber, so reads after it cannot be
         // hoisted by the compiler (it issued read, wait, convert, store R
@@ -467,6 +473,7 @@ __device__ __forceinline__ void tile_body(const uint8_t *src, uint8_t *dst, type
         constexpr int R = S::R, E2 = S::E2;
 #pragma unroll
         for (int k = 0; k < R; k++) {
+            if (!valid) break;
             const int c = k * L + lane;
             alignas(16) uint8_t sb[16];
             alignas(16) uint8_t db[E2 * DS];
@@ -478,15 +485,15 @@ __device__ __forceinline__ void tile_body(const uint8_t *src, uint8_t *dst, type
             *reinterpret_cast<typename VecT<E2 * DS>::type *>(lds + c * E2 * DS) = o;
         }
         __syncthreads();
-        stv<16, NT>(dst + lane * 16, *reinterpret_cast<const typename VecT<16>::type *>(lds + lane * 16));
+        if (valid) stv<16, NT>(dst + lane * 16, *reinterpret_cast<const typename VecT<16>::type *>(lds + lane * 16));
     }
 }
 
-// scalar remainder [e0, n) by the L threads of one block
+// scalar remainder [e0, n) by the L lanes of one tile
 template <class Op, int L = 256>
 __device__ __forceinline__ void scalar_range(const uint8_t *src, uint8_t *dst, int64_t e0, int64_t n,
-                                             typename Op::fill_t fill, bool &bad) {
-    for (int64_t e = e0 + threadIdx.x; e < n; e += L) scalar_elem<Op>(src, dst, e, fill, bad);
+                                             typename Op::fill_t fill, bool &bad, const int lane = threadIdx.x) {
+    for (int64_t e = e0 + lane; e < n; e += L) scalar_elem<Op>(src, dst, e, fill, bad);
 }
 
 template <class Op, bool NT>
@@ -505,7 +512,7 @@ __global__ __launch_bounds__(Shape<Op>::LANES) void k_tile(const uint8_t *src, u
     uint8_t *td = dst + head * S::DS;
     for (int64_t t = xcd_remap(blockIdx.x, nb); t < ntile; t += nb) {
         tile_body<Op, NT>(ts + t * (int64_t)S::TILE * S::SS, td + t * (int64_t)S::TILE * S::DS, fill, bad,
-                          lds);
+                          lds, threadIdx.x, true);
         if constexpr (S::USE_LDS) __syncthreads();       // LDS reuse in the next tile
     }
     publish(sk, sk.status, bad);
@@ -533,28 +540,123 @@ __global__ __launch_bounds__(256) void k_scalar(const uint8_t *src, uint8_t *dst
 // the segment's first block also runs its scalar head and remainder.
 constexpr int BATCH_STEPS = 1;  // tiles per block
 
+// tile b of a batch class: segment lookup, the segment's scalar head and
+// remainder on its first tile, the tile body, and the NC_ERANGE flag of b
 template <class Op, bool NT>
-__global__ __launch_bounds__(Shape<Op>::LANES) void k_batch(const pncxk_seg *segs, int nseg, const int *map,
-                                                            pncxk_groups grp, Sink sk) {
+__device__ __forceinline__ void batch_tile(const pncxk_seg *segs, int nseg, const int *map, const pncxk_groups &grp,
+                                           const Sink &sk, long long b, bool present, int lane, uint8_t *lds) {
     using S = Shape<Op>;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[S::LDS_BYTES];
-    const long long b = batch_block();   // logical block: segment lookup and flag slot
-    const int lo = batch_segment<true>(b, map, grp, segs, nseg);
+    const int lo = present ? batch_segment<true>(b, map, grp, segs, nseg) : 0;
     const pncxk_seg sg = segs[lo];
     const uint8_t *src = (const uint8_t *)sg.src;
     uint8_t *dst = (uint8_t *)sg.dst;
     const typename Op::fill_t fill = sg.fill;
     const int64_t ntile = sg.nvec;     // full tiles
     bool bad = false;
-    const int64_t rel = b - sg.block0;
+    const int64_t rel = present ? b - sg.block0 : -1;
     if (rel == 0) {
-        scalar_range<Op, S::LANES>(src, dst, 0, sg.head, fill, bad);
-        scalar_range<Op, S::LANES>(src, dst, sg.head + ntile * S::TILE, sg.n, fill, bad);
+        scalar_range<Op, S::LANES>(src, dst, 0, sg.head, fill, bad, lane);
+        scalar_range<Op, S::LANES>(src, dst, sg.head + ntile * S::TILE, sg.n, fill, bad, lane);
     }
-    if (rel < ntile)
-        tile_body<Op, NT>(src + (sg.head + rel * (int64_t)S::TILE) * S::SS,
-                          dst + (sg.head + rel * (int64_t)S::TILE) * S::DS, fill, bad, lds);
-    publish(sk, sg.status, bad, b);
+    tile_body<Op, NT>(src + (sg.head + rel * (int64_t)S::TILE) * S::SS,
+                      dst + (sg.head + rel * (int64_t)S::TILE) * S::DS, fill, bad, lds, lane, rel >= 0 && rel < ntile);
+    if (present) publish(sk, sg.status, bad, b);
+}
+
+template <class Op, bool NT>
+__global__ __launch_bounds__(Shape<Op>::LANES) void k_batch(const pncxk_seg *segs, int nseg, const int *map,
+                                                            pncxk_groups grp, Sink sk) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[Shape<Op>::LDS_BYTES];
+    // logical block: segment lookup and flag slot
+    batch_tile<Op, NT>(segs, nseg, map, grp, sk, batch_block(), true, threadIdx.x, lds);
+}
+
+// ---------------------------------------------------------------------------
+// Same-type swaps of a batch (the SWAPMIX class: C4's NC_SHORT and NC_FLOAT
+// iputs): a block of MIX_LANES lanes x 16 B, one nontemporal vector per
+// lane, the element size read from the segment.
+// ---------------------------------------------------------------------------
+constexpr int MIX_LANES = PNCXK_MIX_LANES;
+
+__device__ __forceinline__ u32x4 swap16(u32x4 v, int es) {
+    u32x4 r = v;
+    if (es == 2) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) r[k] = ((v[k] & 0x00ff00ffu) << 8) | ((v[k] >> 8) & 0x00ff00ffu);
+    } else if (es == 4) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) r[k] = __builtin_bswap32(v[k]);
+    } else if (es == 8) {
+        r[0] = __builtin_bswap32(v[1]); r[1] = __builtin_bswap32(v[0]);
+        r[2] = __builtin_bswap32(v[3]); r[3] = __builtin_bswap32(v[2]);
+    }
+    return r;                              // es == 1: copy
+}
+
+template <int ES>
+__device__ __forceinline__ void mix_scalar(const uint8_t *src, uint8_t *dst, int64_t e0, int64_t e1) {
+    using Op = SwapOp<ES>;
+    bool bad = false;
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += MIX_LANES) scalar_elem<Op>(src, dst, e, 0, bad);
+}
+
+__device__ __forceinline__ void mix_block(const pncxk_seg *segs, int nseg, const int *map, const pncxk_groups &grp,
+                                          long long b) {
+    const int s = batch_segment<false>(b, map, grp, segs, nseg);
+    const pncxk_seg sg = segs[s];
+    const uint8_t *src = (const uint8_t *)sg.src;
+    uint8_t *dst = (uint8_t *)sg.dst;
+    const int es = sg.aux;
+    const int64_t rel = b - sg.block0;
+    if (rel < sg.nvec) {
+        const int64_t off = sg.head * es + (rel * MIX_LANES + threadIdx.x) * 16;
+        st16<true>(dst + off, swap16(ld16<true>(src + off), es));
+    }
+    if (rel == 0) {                        // scalar head and remainder (one lane per element)
+        const int64_t tail0 = sg.head + sg.nvec * (int64_t)(MIX_LANES * 16 / es);
+        switch (es) {
+            case 1: mix_scalar<1>(src, dst, 0, sg.head); mix_scalar<1>(src, dst, tail0, sg.n); break;
+            case 2: mix_scalar<2>(src, dst, 0, sg.head); mix_scalar<2>(src, dst, tail0, sg.n); break;
+            case 4: mix_scalar<4>(src, dst, 0, sg.head); mix_scalar<4>(src, dst, tail0, sg.n); break;
+            case 8: mix_scalar<8>(src, dst, 0, sg.head); mix_scalar<8>(src, dst, tail0, sg.n); break;
+            default: break;
+        }
+    }
+    // swaps never produce NC_ERANGE: no status
+}
+
+// One launch for a batch of two classes: a conversion class (256-lane tiles,
+// run four to a block) and the same-type swaps (mix blocks).  Saves the
+// second kernel's ramp and drain (C4's NC_ERANGE variant: float -> NC_SHORT
+// + the NC_FLOAT swaps).  Both classes are spread over all eight XCDs: with
+// the conversion blocks first in one XCD-contiguous grid, two XCDs held
+// 1.5x the bytes of the others and the launch took 0.44 ms against 0.30 ms
+// for the two kernels (each XCD moves about an eighth of the chip's HBM
+// rate).  So block b (round-robin dispatch: XCD x = b % 8, slot j = b / 8)
+// takes, on every XCD, first its share of the conversion blocks, then its
+// share of the swap blocks, each share contiguous (both block counts padded
+// to multiples of 8; padding blocks move nothing).
+constexpr int FUSE_SUB = MIX_LANES / 256;
+
+template <class Op>
+__global__ __launch_bounds__(MIX_LANES) void k_batch_fused(const pncxk_seg *asegs, int anseg, const int *amap,
+                                                           pncxk_groups agrp, long long atiles, long long afused8,
+                                                           const pncxk_seg *bsegs, int bnseg, const int *bmap,
+                                                           pncxk_groups bgrp, long long bblocks, long long bblocks8,
+                                                           Sink sk) {
+    static_assert(Shape<Op>::LANES == 256 && Shape<Op>::PAD_LDS == 0, "fused: uncapped 256-lane tiles");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[FUSE_SUB * Shape<Op>::LDS_BYTES];
+    const long long x = blockIdx.x & 7, j = blockIdx.x >> 3, aper = afused8 >> 3, bper = bblocks8 >> 3;
+    if (j < aper) {                        // block-uniform branch: the tile barriers stay convergent
+        const long long fb = x * aper + j;
+        const int sub = threadIdx.x >> 8;
+        const long long t = fb * FUSE_SUB + sub;
+        batch_tile<Op, true>(asegs, anseg, amap, agrp, sk, t, t < atiles, threadIdx.x & 255,
+                             lds + sub * Shape<Op>::LDS_BYTES);
+    } else {
+        const long long mb = x * bper + (j - aper);
+        if (mb < bblocks) mix_block(bsegs, bnseg, bmap, bgrp, mb);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1072,6 +1174,34 @@ int launch_batch(const pncxk_batch_args *a) {
         hipLaunchKernelGGL((k_batch<Op, true>), dim3((unsigned)a->nblocks), dim3(Shape<Op>::LANES), Shape<Op>::PAD_LDS,
                            st, a->dsegs, a->nseg, a->dmap, a->grp, sk);
     return sink_finish_batch(sk, a->dsegs, a->nseg, a->nblocks, st, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
+}
+
+// one launch for a conversion class `a` and the same-type swap class `m`
+// of one batch (k_batch_fused); PNCXK_NOFUSE when the class's tiles do not
+// fit the fused block (capped occupancy, NULL-fill codecs)
+template <class Op>
+int launch_batch_fused(const pncxk_batch_args *a, const pncxk_batch_args *m) {
+    if constexpr (Op::PRESERVE || Shape<Op>::LANES != 256 || Shape<Op>::PAD_LDS != 0) {
+        return PNCXK_NOFUSE;
+    } else {
+        if (a->nblocks <= 0 || m->nblocks <= 0) return PNCXK_NOFUSE;
+        hipStream_t st = (hipStream_t)a->stream;
+        const long long afused = (a->nblocks + FUSE_SUB - 1) / FUSE_SUB;
+        const long long afused8 = (afused + 7) & ~7LL, bblocks8 = (m->nblocks + 7) & ~7LL;
+        const long long grid = afused8 + bblocks8;
+        const Sink sk = sink_acquire(nullptr, a->sval, st, a->nblocks, may_range<Op>::value);
+        hipEvent_t e0 = (hipEvent_t)a->ev_start, e1 = (hipEvent_t)a->ev_stop;
+        if (e0 != nullptr || e1 != nullptr)
+            hipExtLaunchKernelGGL((k_batch_fused<Op>), dim3((unsigned)grid), dim3(MIX_LANES), 0, st, e0, e1, 0,
+                                  a->dsegs, a->nseg, a->dmap, a->grp, a->nblocks, afused8, m->dsegs, m->nseg, m->dmap,
+                                  m->grp, m->nblocks, bblocks8, sk);
+        else
+            hipLaunchKernelGGL((k_batch_fused<Op>), dim3((unsigned)grid), dim3(MIX_LANES), 0, st, a->dsegs, a->nseg,
+                               a->dmap, a->grp, a->nblocks, afused8, m->dsegs, m->nseg, m->dmap, m->grp, m->nblocks,
+                               bblocks8, sk);
+        return sink_finish_batch(sk, a->dsegs, a->nseg, a->nblocks, st,
+                                 hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
+    }
 }
 
 template <class Op>

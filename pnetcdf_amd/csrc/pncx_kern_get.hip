@@ -17,6 +17,11 @@ int get_batch(const pncxk_batch_args *a) {
     else return launch_batch<GetOp<XT, IT>>(a);
 }
 template <int XT, int IT>
+int get_fused(const pncxk_batch_args *a, const pncxk_batch_args *m) {
+    if constexpr (same_rep<XT, IT>::value) return NC_EINVAL;
+    else return launch_batch_fused<GetOp<XT, IT>>(a, m);
+}
+template <int XT, int IT>
 int get_info(pncxk_opinfo *o) {
     OpInfo<GetOp<XT, IT>>::fill(o);
     return 0;
@@ -37,6 +42,15 @@ extern "C" int pncxk_get(int xtype, int itype, const pncxk_args *a) {
 extern "C" int pncxk_batch_get(int xtype, int itype, const pncxk_batch_args *a) {
     switch (PNCX_KEY(xtype, itype)) {
 #define CASE(XT, IT) case PNCX_KEY(XT, IT): return get_batch<XT, IT>(a);
+        PNCX_ALL_PAIRS(CASE)
+#undef CASE
+        default: return NC_EBADTYPE;
+    }
+}
+
+extern "C" int pncxk_batch_fused_get(int xtype, int itype, const pncxk_batch_args *a, const pncxk_batch_args *m) {
+    switch (PNCX_KEY(xtype, itype)) {
+#define CASE(XT, IT) case PNCX_KEY(XT, IT): return get_fused<XT, IT>(a, m);
         PNCX_ALL_PAIRS(CASE)
 #undef CASE
         default: return NC_EBADTYPE;

@@ -29,6 +29,12 @@ int put_batch(int preserve, const pncxk_batch_args *a) {
     }
 }
 template <int XT, int IT>
+int put_fused(int preserve, const pncxk_batch_args *a, const pncxk_batch_args *m) {
+    if constexpr (same_rep<XT, IT>::value) return NC_EINVAL;
+    else if (preserve) return PNCXK_NOFUSE;
+    else return launch_batch_fused<PutOp<XT, IT, false>>(a, m);
+}
+template <int XT, int IT>
 int put_info(pncxk_opinfo *o) {
     OpInfo<PutOp<XT, IT, false>>::fill(o);
     return 0;
@@ -49,6 +55,16 @@ extern "C" int pncxk_put(int xtype, int itype, int preserve, const pncxk_args *a
 extern "C" int pncxk_batch_put(int xtype, int itype, int preserve, const pncxk_batch_args *a) {
     switch (PNCX_KEY(xtype, itype)) {
 #define CASE(XT, IT) case PNCX_KEY(XT, IT): return put_batch<XT, IT>(preserve, a);
+        PNCX_ALL_PAIRS(CASE)
+#undef CASE
+        default: return NC_EBADTYPE;
+    }
+}
+
+extern "C" int pncxk_batch_fused_put(int xtype, int itype, int preserve, const pncxk_batch_args *a,
+                                     const pncxk_batch_args *m) {
+    switch (PNCX_KEY(xtype, itype)) {
+#define CASE(XT, IT) case PNCX_KEY(XT, IT): return put_fused<XT, IT>(preserve, a, m);
         PNCX_ALL_PAIRS(CASE)
 #undef CASE
         default: return NC_EBADTYPE;

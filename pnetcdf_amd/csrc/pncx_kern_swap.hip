@@ -289,68 +289,21 @@ extern "C" int pncxk_batch_get(int xtype, int itype, const pncxk_batch_args *a);
 extern "C" int pncxk_batch_put(int xtype, int itype, int preserve, const pncxk_batch_args *a);
 extern "C" int pncxk_opinfo_getput(int kind, int xtype, int itype, int preserve, pncxk_opinfo *o);
 
-constexpr int MIX_LANES = PNCXK_MIX_LANES;
-
 // One launch for all same-type segments of a batch (C4: NC_SHORT and
-// NC_FLOAT iputs): the block's segment says its element size.  A block is
-// MIX_LANES lanes x 16 B (one nontemporal vector each, no loop), blocks in
-// XCD-contiguous order.  Round 2 (tools/c4_shape_sweep.hip, 256 buffer pairs,
-// splitmix64 data, three boxes): launch order at 1024 lanes 75.8-77.1 % of
-// peak, XCD-contiguous order 80.3-82.7 % at 256, 512 or 1024 lanes; the same
-// descriptors pointing into one allocation per side 83.3-84.1 %, one flat
-// buffer pair 83.4-84.5 %.  Two or four vectors per lane lose 1-5 points.
-// Plain (write-back) stores lose 1-4 points to "nt sc1" in the library
-// (tools/c4_placement.py); persistent grids that prefetch their next tile
-// ran at 65-74 % (tools/c4_store_sweep.hip).
-__device__ __forceinline__ u32x4 swap16(u32x4 v, int es) {
-    u32x4 r = v;
-    if (es == 2) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) r[k] = ((v[k] & 0x00ff00ffu) << 8) | ((v[k] >> 8) & 0x00ff00ffu);
-    } else if (es == 4) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) r[k] = __builtin_bswap32(v[k]);
-    } else if (es == 8) {
-        r[0] = __builtin_bswap32(v[1]); r[1] = __builtin_bswap32(v[0]);
-        r[2] = __builtin_bswap32(v[3]); r[3] = __builtin_bswap32(v[2]);
-    }
-    return r;                              // es == 1: copy
-}
-
-template <int ES>
-__device__ __forceinline__ void mix_scalar(const uint8_t *src, uint8_t *dst, int64_t e0, int64_t e1) {
-    using Op = SwapOp<ES>;
-    bool bad = false;
-    for (int64_t e = e0 + threadIdx.x; e < e1; e += MIX_LANES) scalar_elem<Op>(src, dst, e, 0, bad);
-}
-
+// NC_FLOAT iputs): the block's segment says its element size (mix_block,
+// pncx_kern.hpp).  A block is MIX_LANES lanes x 16 B (one nontemporal vector
+// each, no loop), blocks in XCD-contiguous order.  Round 2
+// (tools/c4_shape_sweep.hip, 256 buffer pairs, splitmix64 data, three
+// boxes): launch order at 1024 lanes 75.8-77.1 % of peak, XCD-contiguous
+// order 80.3-82.7 % at 256, 512 or 1024 lanes; the same descriptors pointing
+// into one allocation per side 83.3-84.1 %, one flat buffer pair 83.4-84.5 %.
+// Two or four vectors per lane lose 1-5 points.  Plain (write-back) stores
+// lose 1-4 points to "nt sc1" in the library (tools/c4_placement.py);
+// persistent grids that prefetch their next tile ran at 65-74 %
+// (tools/c4_store_sweep.hip).
 __global__ __launch_bounds__(MIX_LANES) void k_batch_swapmix(const pncxk_seg *segs, int nseg, const int *map,
                                                              pncxk_groups grp) {
-    // XCD-contiguous block order (each XCD takes one contiguous run of
-    // tiles): 75.8-77.1 % -> 80.3-82.7 % of peak on the C4 layout at 1024
-    // lanes, three boxes (tools/c4_shape_sweep.hip, profiles/r02_c4_shape_sweep*.txt)
-    const long long b = batch_block();
-    const int s = batch_segment<false>(b, map, grp, segs, nseg);
-    const pncxk_seg sg = segs[s];
-    const uint8_t *src = (const uint8_t *)sg.src;
-    uint8_t *dst = (uint8_t *)sg.dst;
-    const int es = sg.aux;
-    const int64_t rel = b - sg.block0;
-    if (rel < sg.nvec) {
-        const int64_t off = sg.head * es + (rel * MIX_LANES + threadIdx.x) * 16;
-        st16<true>(dst + off, swap16(ld16<true>(src + off), es));
-    }
-    if (rel == 0) {                        // scalar head and remainder (one lane per element)
-        const int64_t tail0 = sg.head + sg.nvec * (int64_t)(MIX_LANES * 16 / es);
-        switch (es) {
-            case 1: mix_scalar<1>(src, dst, 0, sg.head); mix_scalar<1>(src, dst, tail0, sg.n); break;
-            case 2: mix_scalar<2>(src, dst, 0, sg.head); mix_scalar<2>(src, dst, tail0, sg.n); break;
-            case 4: mix_scalar<4>(src, dst, 0, sg.head); mix_scalar<4>(src, dst, tail0, sg.n); break;
-            case 8: mix_scalar<8>(src, dst, 0, sg.head); mix_scalar<8>(src, dst, tail0, sg.n); break;
-            default: break;
-        }
-    }
-    // swaps never produce NC_ERANGE: no status
+    mix_block(segs, nseg, map, grp, batch_block());
 }
 
 extern "C" int pncxk_batch(int kind, int a, int b, int c, const pncxk_batch_args *args) {
@@ -378,6 +331,17 @@ extern "C" int pncxk_batch(int kind, int a, int b, int c, const pncxk_batch_args
     if (kind == PNCXK_GET) return pncxk_batch_get(a, b, args);
     if (kind == PNCXK_PUT) return pncxk_batch_put(a, b, c, args);
     return NC_EINVAL;
+}
+
+extern "C" int pncxk_batch_fused_get(int xtype, int itype, const pncxk_batch_args *a, const pncxk_batch_args *m);
+extern "C" int pncxk_batch_fused_put(int xtype, int itype, int preserve, const pncxk_batch_args *a,
+                                     const pncxk_batch_args *m);
+
+extern "C" int pncxk_batch_fused(int kind, int a, int b, int c, const pncxk_batch_args *conv,
+                                 const pncxk_batch_args *mix) {
+    if (kind == PNCXK_GET) return pncxk_batch_fused_get(a, b, conv, mix);
+    if (kind == PNCXK_PUT) return pncxk_batch_fused_put(a, b, c, conv, mix);
+    return PNCXK_NOFUSE;
 }
 
 // block -> segment table for non-uniform batches: block s of this grid

@@ -127,6 +127,11 @@ int pncxk_swap_generic(int esize, const pncxk_args *a);  /* any esize >= 1 */
 int pncxk_get(int xtype, int itype, const pncxk_args *a);
 int pncxk_put(int xtype, int itype, int preserve, const pncxk_args *a);
 int pncxk_batch(int kind, int a, int b, int c, const pncxk_batch_args *args);
+/* one launch for a conversion class (conv) and the same-type swap class
+ * (mix) of one batch; PNCXK_NOFUSE when the pair does not fuse (then the
+ * caller launches both classes itself) */
+#define PNCXK_NOFUSE 1
+int pncxk_batch_fused(int kind, int a, int b, int c, const pncxk_batch_args *conv, const pncxk_batch_args *mix);
 /* fused varm gather (gather=1: put, src strided) / scatter (get, dst strided) */
 int pncxk_launch_imap(int kind, int a, int b, int c, const pncxk_args *args, const pncxk_imap *m, int gather);
 int pncxk_opinfo_get(int kind, int a, int b, int c, pncxk_opinfo *o);

@@ -345,6 +345,28 @@ def dev_getn(cdf_ver, xtype, dx, di, nelems, itype, dstatus=None, stream=None):
            "dev_getn", (T.NC_NOERR,))
 
 
+def _dev_segs(segs):
+    arr = (Seg * len(segs))()
+    keep = []
+    for k, s in enumerate(segs):
+        fb = None
+        if s.get("fill") is not None:
+            fb = np.frombuffer(bytes(s["fill"]) + b"\0" * 8, np.uint8).copy()
+            keep.append(fb)
+        arr[k] = Seg(s["dir"], s.get("cdf_ver", 5), s["xtype"], s["itype"], s["nelems"],
+                     s["xbuf"].data_ptr(), s["ibuf"].data_ptr(),
+                     None if fb is None else fb.ctypes.data)
+    return arr, keep
+
+
+def dev_batch_async(segs, dstatus, stream=None):
+    """pncx_dev_batch_async: the statuses land in the int32 CUDA tensor
+    `dstatus` (NC_ERANGE words) once the stream gets there; returns the
+    call's code (the fill values are copied during the call)."""
+    arr, keep = _dev_segs(segs)
+    return lib().pncx_dev_batch_async(arr, len(segs), _dptr(dstatus), _stream_ptr(stream))
+
+
 def dev_batch(segs, stream=None):
     """Device batch: like ``batch`` but xbuf/ibuf are CUDA tensors."""
     arr = (Seg * len(segs))()

@@ -719,7 +719,7 @@ def test_large_conversions_every_element(torch_cuda):
         assert torch.equal(of, f), rep
 
 
-def _fuzz_segments(torch, rng, ora, nseg):
+def _fuzz_segments(torch, rng, ora, nseg, pairs=None, dirs=None):
     """Random segments over every (cdf, xtype, itype) pair and both directions:
     sizes 0..40000 (a few large), byte offsets 0..15 on both buffers, put
     fills that are the default, a user value or NULL (the existing external
@@ -732,8 +732,13 @@ def _fuzz_segments(torch, rng, ora, nseg):
 
     segs, refs = [], []
     for _ in range(nseg):
-        cdf, xt, it, _k = PAIRS[int(rng.integers(0, len(PAIRS)))]
-        d = T.PNCX_GET if rng.random() < 0.5 else T.PNCX_PUT
+        if pairs is None:
+            cdf, xt, it, _k = PAIRS[int(rng.integers(0, len(PAIRS)))]
+            d = T.PNCX_GET if rng.random() < 0.5 else T.PNCX_PUT
+        else:
+            j = int(rng.integers(0, len(pairs)))
+            cdf, xt, it = pairs[j]
+            d = dirs[j]
         n = int(rng.integers(0, 40000)) if rng.random() < 0.9 else int(rng.integers(200000, 600000))
         ox, oi = int(rng.integers(0, 16)), int(rng.integers(0, 16))
         xs, isz = T.xlen(xt), T.ilen(it)
@@ -778,6 +783,47 @@ def _reset_outputs(torch, refs):
         buf[off:off + nb] = 0
         if xinit:
             buf[off:off + nb] = torch.frombuffer(bytearray(xinit), dtype=torch.uint8).cuda()
+
+
+# (direction, xtype, itype) of the conversion class beside the same-type
+# swaps: the C4 NC_ERANGE variant, a direct class, LDS narrowing and
+# widening tiles, and an 8:1 class whose capped occupancy does not fuse
+FUSE_CLASSES = [(T.PNCX_PUT, T.NC_SHORT, T.ITYPE_FLOAT), (T.PNCX_GET, T.NC_INT, T.ITYPE_DOUBLE),
+                (T.PNCX_PUT, T.NC_FLOAT, T.ITYPE_DOUBLE), (T.PNCX_GET, T.NC_BYTE, T.ITYPE_SHORT),
+                (T.PNCX_GET, T.NC_SHORT, T.ITYPE_DOUBLE), (T.PNCX_GET, T.NC_DOUBLE, T.ITYPE_SCHAR)]
+
+
+@pytest.mark.parametrize("cls", FUSE_CLASSES, ids=lambda c: f"{'get' if c[0] == T.PNCX_GET else 'put'}_"
+                         f"{T.XNAME[c[1]]}_{T.INAME[c[2]]}")
+@pytest.mark.parametrize("seed", [1, 2])
+def test_dev_batch_fused_two_classes(torch_cuda, cls, seed):
+    """A batch of exactly one conversion class and same-type swaps runs as
+    ONE fused launch (k_batch_fused: four 256-lane conversion tiles per block,
+    then the swap blocks; a class with capped occupancy falls back to two
+    launches).  Random sizes (tile counts not multiples of four, scalar heads
+    and tails), offsets, fills and NC_ERANGE: bit-exact against the oracle,
+    synchronous (twice, the second from the plan cache) and asynchronous."""
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    ora = OracleConv()
+    rng = np.random.default_rng(0xF05E + seed)
+    d, xt, it = cls
+    swaps = [(5, T.NC_FLOAT, T.ITYPE_FLOAT), (5, T.NC_SHORT, T.ITYPE_SHORT), (5, T.NC_DOUBLE, T.ITYPE_DOUBLE),
+             (5, T.NC_INT, T.ITYPE_INT)]
+    pairs = [(5, xt, it)] * 4 + swaps
+    dirs = [d] * 4 + [T.PNCX_PUT, T.PNCX_GET, T.PNCX_PUT, T.PNCX_GET]
+    segs, refs = _fuzz_segments(torch, rng, ora, 40, pairs, dirs)
+    _check_refs(refs, pncx.dev_batch(segs))
+    _reset_outputs(torch, refs)
+    _check_refs(refs, pncx.dev_batch(segs))
+    _reset_outputs(torch, refs)
+    dst = torch.zeros(len(segs), dtype=torch.int32, device="cuda")
+    assert pncx.dev_batch_async(segs, dst) == 0
+    torch.cuda.synchronize()
+    want = [r[3] for r in refs]
+    assert dst.cpu().tolist() == want
+    for k, (buf, off, exp, so, nb, _x) in enumerate(refs):
+        assert buf[off:off + nb].cpu().numpy().tobytes() == exp, k
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])

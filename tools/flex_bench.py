@@ -28,7 +28,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--big", action="store_true",
+                    help="every workload at >= 4 GiB moved per launch (2^28 elements and more)")
     args = ap.parse_args()
+    big = args.big
     import torch
     from pnetcdf_amd import nctypes as T
     from pnetcdf_amd import pncx
@@ -59,8 +62,8 @@ def main():
         return ms, n * 16 / ms / 1e6
 
     res = []
-    # halo3d: 256^3 local array, interior 254^3
-    L, I = 256, 254
+    # halo3d: 256^3 local array, interior 254^3 (--big: 648^3, interior 646^3)
+    L, I = (648, 646) if big else (256, 254)
     ub = torch.empty(L ** 3 * 8, dtype=torch.uint8, device="cuda")
     ub.view(torch.float64).normal_()
     z, y = np.meshgrid(np.arange(I), np.arange(I), indexing="ij")
@@ -75,9 +78,9 @@ def main():
     res.append(("contig", -1, n) + timeit(
         lambda: lib.pncx_dev_putn(5, T.NC_DOUBLE, ctypes.c_void_p(xb.data_ptr()), ctypes.c_void_p(ub.data_ptr()), n,
                                   T.ITYPE_DOUBLE, fp, ctypes.c_void_p(st.data_ptr()), sp), n))
-    # vector2 / vector64 over 2^27 elements
+    # vector2 / vector64 over 2^27 elements (--big: 2^28)
     for name, blen, stride in (("vector2", 1, 2), ("vector64", 64, 80), ("vector256", 256, 272)):
-        nb = (1 << 27) // blen
+        nb = (1 << (28 if big else 27)) // blen
         span = nb * stride * 8
         u2 = torch.empty(span, dtype=torch.uint8, device="cuda")
         dtv = pncx.DType(T.ITYPE_DOUBLE, (np.arange(nb, dtype=np.int64) * stride * 8).tolist(), [blen] * nb, span)
@@ -91,7 +94,7 @@ def main():
         del u2, x2
     # short irregular runs (1..7 elements, gaps 0..4): per-element table search
     rng = np.random.default_rng(5)
-    nb = 1 << 20
+    nb = 1 << (23 if big else 20)
     blen = rng.integers(1, 8, nb)
     disp = np.concatenate([[0], np.cumsum(blen + rng.integers(0, 5, nb))[:-1]]).astype(np.int64) * 8
     span = int(disp[-1]) + int(blen[-1]) * 8
@@ -111,9 +114,9 @@ def main():
                                        1, cp4, None, 8, dts2.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n4))
     del u4, x4
     # transpose varm
-    cnt = [512, 512, 128]
-    imap = [1, 512, 512 * 512]
-    n3 = 512 * 512 * 128
+    cnt = [1024, 1024, 256] if big else [512, 512, 128]
+    imap = [1, cnt[0], cnt[0] * cnt[1]]
+    n3 = cnt[0] * cnt[1] * cnt[2]
     u3 = torch.empty(n3 * 8, dtype=torch.uint8, device="cuda")
     x3 = torch.empty(n3 * 8, dtype=torch.uint8, device="cuda")
     c3, cp3 = offs(cnt)
@@ -122,7 +125,8 @@ def main():
         lambda: lib.pncx_dev_putn_imap(5, T.NC_DOUBLE, ctypes.c_void_p(x3.data_ptr()), ctypes.c_void_p(u3.data_ptr()),
                                        3, cp3, mp3, T.ITYPE_DOUBLE, fp, ctypes.c_void_p(st.data_ptr()), sp), n3))
     # the same transpose with non-power-of-two extents (strides off the channel interleave)
-    for cnt in ([500, 500, 120], [512, 512, 120], [500, 512, 128]):
+    for cnt in (([1000, 1000, 268], [1024, 1024, 250], [1000, 1024, 256]) if big else
+                ([500, 500, 120], [512, 512, 120], [500, 512, 128])):
         imap = [1, cnt[0], cnt[0] * cnt[1]]
         n5 = cnt[0] * cnt[1] * cnt[2]
         u5 = torch.empty(n5 * 8, dtype=torch.uint8, device="cuda")
