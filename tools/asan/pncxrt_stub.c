@@ -40,6 +40,8 @@ int pncxk_swap_generic(int e, const pncxk_args *a) { (void)e; (void)a; return NO
 int pncxk_get(int x, int i, const pncxk_args *a) { (void)x; (void)i; (void)a; return NODEV; }
 int pncxk_put(int x, int i, int p, const pncxk_args *a) { (void)x; (void)i; (void)p; (void)a; return NODEV; }
 int pncxk_batch(int k, int a, int b, int c, const pncxk_batch_args *x) { (void)k; (void)a; (void)b; (void)c; (void)x; return NODEV; }
+int pncxk_batch_fused(int k, int a, int b, int c, const pncxk_batch_args *x, const pncxk_batch_args *y)
+{ (void)k; (void)a; (void)b; (void)c; (void)x; (void)y; return NODEV; }
 int pncxk_launch_imap(int k, int a, int b, int c, const pncxk_args *x, const pncxk_imap *m, int g)
 { (void)k; (void)a; (void)b; (void)c; (void)x; (void)m; (void)g; return NODEV; }
 int pncxk_opinfo_get(int k, int a, int b, int c, pncxk_opinfo *o) { (void)k; (void)a; (void)b; (void)c; (void)o; return NODEV; }
