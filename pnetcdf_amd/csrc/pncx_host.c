@@ -1402,15 +1402,17 @@ static void batch_time(ctx_t *c)
     c->tcpend++;
 }
 
-/* PNCX_BATCH_FUSE=0 launches every class of a batch on its own (A/B) */
+/* PNCX_BATCH_FUSE=1 runs a conversion class and the same-type swaps of one
+ * batch as one launch (k_batch_fused).  Off by default: on C4's NC_ERANGE
+ * variant the fused launch took 0.3026-0.3032 ms with 256-lane blocks and
+ * 0.3160-0.3169 ms with 1024-lane blocks against 0.2995-0.3007 ms for the
+ * two class kernels, in alternating runs on one box
+ * (profiles/r03_fuse_ab.txt): the ramp and drain it saves are not where
+ * the time goes.  Read per call, so tests can run both ways in one process. */
 static int batch_fuse_enabled(void)
 {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("PNCX_BATCH_FUSE");
-        v = e == NULL || atoi(e) != 0;
-    }
-    return v;
+    const char *e = getenv("PNCX_BATCH_FUSE");
+    return e != NULL && atoi(e) != 0;
 }
 
 /* launch the class kernels of a plan whose descriptors are on the device */

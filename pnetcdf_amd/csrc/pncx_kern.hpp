@@ -593,15 +593,18 @@ __device__ __forceinline__ u32x4 swap16(u32x4 v, int es) {
     return r;                              // es == 1: copy
 }
 
-template <int ES>
+template <int ES, int L = MIX_LANES>
 __device__ __forceinline__ void mix_scalar(const uint8_t *src, uint8_t *dst, int64_t e0, int64_t e1) {
     using Op = SwapOp<ES>;
     bool bad = false;
-    for (int64_t e = e0 + threadIdx.x; e < e1; e += MIX_LANES) scalar_elem<Op>(src, dst, e, 0, bad);
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += L) scalar_elem<Op>(src, dst, e, 0, bad);
 }
 
+// part `sub` of mix block b, run by L = MIX_LANES / parts lanes (the plan's
+// block b covers MIX_LANES x 16 B; a smaller block covers a slice of it)
+template <int L = MIX_LANES>
 __device__ __forceinline__ void mix_block(const pncxk_seg *segs, int nseg, const int *map, const pncxk_groups &grp,
-                                          long long b) {
+                                          long long b, int sub = 0) {
     const int s = batch_segment<false>(b, map, grp, segs, nseg);
     const pncxk_seg sg = segs[s];
     const uint8_t *src = (const uint8_t *)sg.src;
@@ -609,53 +612,56 @@ __device__ __forceinline__ void mix_block(const pncxk_seg *segs, int nseg, const
     const int es = sg.aux;
     const int64_t rel = b - sg.block0;
     if (rel < sg.nvec) {
-        const int64_t off = sg.head * es + (rel * MIX_LANES + threadIdx.x) * 16;
+        const int64_t off = sg.head * es + (rel * MIX_LANES + sub * L + threadIdx.x) * 16;
         st16<true>(dst + off, swap16(ld16<true>(src + off), es));
     }
-    if (rel == 0) {                        // scalar head and remainder (one lane per element)
+    if (rel == 0 && sub == 0) {            // scalar head and remainder (one lane per element)
         const int64_t tail0 = sg.head + sg.nvec * (int64_t)(MIX_LANES * 16 / es);
         switch (es) {
-            case 1: mix_scalar<1>(src, dst, 0, sg.head); mix_scalar<1>(src, dst, tail0, sg.n); break;
-            case 2: mix_scalar<2>(src, dst, 0, sg.head); mix_scalar<2>(src, dst, tail0, sg.n); break;
-            case 4: mix_scalar<4>(src, dst, 0, sg.head); mix_scalar<4>(src, dst, tail0, sg.n); break;
-            case 8: mix_scalar<8>(src, dst, 0, sg.head); mix_scalar<8>(src, dst, tail0, sg.n); break;
+            case 1: mix_scalar<1, L>(src, dst, 0, sg.head); mix_scalar<1, L>(src, dst, tail0, sg.n); break;
+            case 2: mix_scalar<2, L>(src, dst, 0, sg.head); mix_scalar<2, L>(src, dst, tail0, sg.n); break;
+            case 4: mix_scalar<4, L>(src, dst, 0, sg.head); mix_scalar<4, L>(src, dst, tail0, sg.n); break;
+            case 8: mix_scalar<8, L>(src, dst, 0, sg.head); mix_scalar<8, L>(src, dst, tail0, sg.n); break;
             default: break;
         }
     }
     // swaps never produce NC_ERANGE: no status
 }
 
-// One launch for a batch of two classes: a conversion class (256-lane tiles,
-// run four to a block) and the same-type swaps (mix blocks).  Saves the
-// second kernel's ramp and drain (C4's NC_ERANGE variant: float -> NC_SHORT
-// + the NC_FLOAT swaps).  Both classes are spread over all eight XCDs: with
-// the conversion blocks first in one XCD-contiguous grid, two XCDs held
-// 1.5x the bytes of the others and the launch took 0.44 ms against 0.30 ms
-// for the two kernels (each XCD moves about an eighth of the chip's HBM
-// rate).  So block b (round-robin dispatch: XCD x = b % 8, slot j = b / 8)
-// takes, on every XCD, first its share of the conversion blocks, then its
-// share of the swap blocks, each share contiguous (both block counts padded
-// to multiples of 8; padding blocks move nothing).
-constexpr int FUSE_SUB = MIX_LANES / 256;
-
-template <class Op>
-__global__ __launch_bounds__(MIX_LANES) void k_batch_fused(const pncxk_seg *asegs, int anseg, const int *amap,
-                                                           pncxk_groups agrp, long long atiles, long long afused8,
-                                                           const pncxk_seg *bsegs, int bnseg, const int *bmap,
-                                                           pncxk_groups bgrp, long long bblocks, long long bblocks8,
-                                                           Sink sk) {
+// One launch for a batch of two classes: a conversion class (256-lane tiles)
+// and the same-type swaps (mix blocks).  Saves the second kernel's ramp and
+// drain (C4's NC_ERANGE variant: float -> NC_SHORT + the NC_FLOAT swaps).
+// Both classes are spread over all eight XCDs: with the conversion blocks
+// first in one XCD-contiguous grid, two XCDs held 1.5x the bytes of the
+// others and the launch took 0.44 ms against 0.30 ms for the two kernels
+// (each XCD moves about an eighth of the chip's HBM rate).  So block b
+// (round-robin dispatch: XCD x = b % 8, slot j = b / 8) takes, on every XCD,
+// first its share of the conversion units, then its share of the swap units,
+// each share contiguous (both unit counts padded to multiples of 8; padding
+// blocks move nothing).
+//   FL = 1024: a block runs four conversion tiles (one LDS barrier over 16
+//              waves) or one whole mix block;
+//   FL = 256:  a block runs one conversion tile, as k_batch does, or a
+//              quarter of a mix block.
+template <class Op, int FL>
+__global__ __launch_bounds__(FL) void k_batch_fused(const pncxk_seg *asegs, int anseg, const int *amap,
+                                                    pncxk_groups agrp, long long atiles, long long aunits8,
+                                                    const pncxk_seg *bsegs, int bnseg, const int *bmap,
+                                                    pncxk_groups bgrp, long long bblocks, long long bunits8,
+                                                    Sink sk) {
     static_assert(Shape<Op>::LANES == 256 && Shape<Op>::PAD_LDS == 0, "fused: uncapped 256-lane tiles");
-    __shared__ __attribute__((aligned(16))) uint8_t lds[FUSE_SUB * Shape<Op>::LDS_BYTES];
-    const long long x = blockIdx.x & 7, j = blockIdx.x >> 3, aper = afused8 >> 3, bper = bblocks8 >> 3;
+    constexpr int ASUB = FL / 256, BSUB = MIX_LANES / FL;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[ASUB * Shape<Op>::LDS_BYTES];
+    const long long x = blockIdx.x & 7, j = blockIdx.x >> 3, aper = aunits8 >> 3, bper = bunits8 >> 3;
     if (j < aper) {                        // block-uniform branch: the tile barriers stay convergent
         const long long fb = x * aper + j;
-        const int sub = threadIdx.x >> 8;
-        const long long t = fb * FUSE_SUB + sub;
+        const int sub = ASUB > 1 ? threadIdx.x >> 8 : 0;
+        const long long t = fb * ASUB + sub;
         batch_tile<Op, true>(asegs, anseg, amap, agrp, sk, t, t < atiles, threadIdx.x & 255,
                              lds + sub * Shape<Op>::LDS_BYTES);
     } else {
-        const long long mb = x * bper + (j - aper);
-        if (mb < bblocks) mix_block(bsegs, bnseg, bmap, bgrp, mb);
+        const long long q = x * bper + (j - aper);
+        if (q < bblocks * BSUB) mix_block<FL>(bsegs, bnseg, bmap, bgrp, q / BSUB, (int)(q % BSUB));
     }
 }
 
@@ -1176,6 +1182,25 @@ int launch_batch(const pncxk_batch_args *a) {
     return sink_finish_batch(sk, a->dsegs, a->nseg, a->nblocks, st, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
 }
 
+// block size of the fused batch launch: PNCX_FUSE_LANES=1024 or 256 (default)
+int fuse_lanes();
+
+template <class Op, int FL>
+void launch_fused(const pncxk_batch_args *a, const pncxk_batch_args *m, const Sink &sk, hipEvent_t e0, hipEvent_t e1,
+                  hipStream_t st) {
+    constexpr int ASUB = FL / 256, BSUB = MIX_LANES / FL;
+    const long long aunits = (a->nblocks + ASUB - 1) / ASUB;
+    const long long aunits8 = (aunits + 7) & ~7LL, bunits8 = (m->nblocks * BSUB + 7) & ~7LL;
+    const long long grid = aunits8 + bunits8;
+    if (e0 != nullptr || e1 != nullptr)
+        hipExtLaunchKernelGGL((k_batch_fused<Op, FL>), dim3((unsigned)grid), dim3(FL), 0, st, e0, e1, 0, a->dsegs,
+                              a->nseg, a->dmap, a->grp, a->nblocks, aunits8, m->dsegs, m->nseg, m->dmap, m->grp,
+                              m->nblocks, bunits8, sk);
+    else
+        hipLaunchKernelGGL((k_batch_fused<Op, FL>), dim3((unsigned)grid), dim3(FL), 0, st, a->dsegs, a->nseg, a->dmap,
+                           a->grp, a->nblocks, aunits8, m->dsegs, m->nseg, m->dmap, m->grp, m->nblocks, bunits8, sk);
+}
+
 // one launch for a conversion class `a` and the same-type swap class `m`
 // of one batch (k_batch_fused); PNCXK_NOFUSE when the class's tiles do not
 // fit the fused block (capped occupancy, NULL-fill codecs)
@@ -1186,19 +1211,12 @@ int launch_batch_fused(const pncxk_batch_args *a, const pncxk_batch_args *m) {
     } else {
         if (a->nblocks <= 0 || m->nblocks <= 0) return PNCXK_NOFUSE;
         hipStream_t st = (hipStream_t)a->stream;
-        const long long afused = (a->nblocks + FUSE_SUB - 1) / FUSE_SUB;
-        const long long afused8 = (afused + 7) & ~7LL, bblocks8 = (m->nblocks + 7) & ~7LL;
-        const long long grid = afused8 + bblocks8;
         const Sink sk = sink_acquire(nullptr, a->sval, st, a->nblocks, may_range<Op>::value);
         hipEvent_t e0 = (hipEvent_t)a->ev_start, e1 = (hipEvent_t)a->ev_stop;
-        if (e0 != nullptr || e1 != nullptr)
-            hipExtLaunchKernelGGL((k_batch_fused<Op>), dim3((unsigned)grid), dim3(MIX_LANES), 0, st, e0, e1, 0,
-                                  a->dsegs, a->nseg, a->dmap, a->grp, a->nblocks, afused8, m->dsegs, m->nseg, m->dmap,
-                                  m->grp, m->nblocks, bblocks8, sk);
+        if (fuse_lanes() == 1024)
+            launch_fused<Op, 1024>(a, m, sk, e0, e1, st);
         else
-            hipLaunchKernelGGL((k_batch_fused<Op>), dim3((unsigned)grid), dim3(MIX_LANES), 0, st, a->dsegs, a->nseg,
-                               a->dmap, a->grp, a->nblocks, afused8, m->dsegs, m->nseg, m->dmap, m->grp, m->nblocks,
-                               bblocks8, sk);
+            launch_fused<Op, 256>(a, m, sk, e0, e1, st);
         return sink_finish_batch(sk, a->dsegs, a->nseg, a->nblocks, st,
                                  hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
     }

@@ -4,6 +4,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <pthread.h>
+
 #include <mutex>
 
 #include "pncx_kern.hpp"
@@ -133,39 +135,76 @@ extern "C" int pncxk_fill(void *dst, long long nelems, int xsize, const void *xv
 
 // ---------------------------------------------------------------------------
 // NC_ERANGE reporting through per-block flags (see Sink in pncx_kern.hpp).
-// A flag array belongs to one (device, stream): calls on one stream run in
-// order, so each call's epoch is new to its array and no zeroing is needed;
-// calls on different streams never share an array (sharing one would let a
-// later call overwrite an earlier call's flags before its reduce reads them).
+// A flag array belongs to one (device, stream[, thread]): calls on one stream
+// run in order, so each call's epoch is new to its array and no zeroing is
+// needed; calls on different streams never share an array (sharing one would
+// let a later call overwrite an earlier call's flags before its reduce reads
+// them).  hipStreamPerThread is one handle for many streams (one per host
+// thread), so its slots are also keyed by the calling thread.
 // The mutex is held from sink_acquire to sink_finish so that one call's
-// kernel and reduce are enqueued back to back.
+// kernel and reduce are enqueued back to back; nothing waits on the device
+// while it is held.
 // No event marks a reduce's completion: an event recorded after every reduce
 // delayed the next kernel on the stream by 5.8 us (the synchronous batch's
-// completion kernel, profiles/r02s_c4_erange trace).  A slot handed to
-// another stream or device, or regrown, is first drained with a device (or
-// stream) synchronize instead -- rare: it takes more than NFLAGSLOT streams.
+// completion kernel, profiles/r02s_c4_erange trace).  So an array can only be
+// known unread once its device has drained: a slot taken over by another
+// stream (more than NFLAGSLOT streams in use) or regrown gets a fresh zeroed
+// array, and the old one is retired and freed after the mutex is released
+// (hipFree drains the device itself).
 // ---------------------------------------------------------------------------
 namespace {
 struct FlagSlot {
     int dev;
     hipStream_t stream;
+    pthread_t thread;     // the owning thread, for hipStreamPerThread only
     int *flags;
     int64_t cap;          // ints
     int epoch;
     uint64_t tick;
     bool live;
 };
+struct Retired {
+    int dev;
+    int *flags;
+};
 constexpr int NFLAGSLOT = 32;
+constexpr int NRETIRE = 2 * NFLAGSLOT;
 FlagSlot g_fslot[NFLAGSLOT];
+Retired g_retired[NRETIRE];
+int g_nretired;
 std::mutex g_fslot_mu;
 uint64_t g_ftick;
 
-// every kernel queued on the slot's device has finished (its stream may be
-// gone, so the whole device is drained)
-void drain_device(int dev, int cur) {
-    if (dev != cur) (void)hipSetDevice(dev);
-    (void)hipDeviceSynchronize();
-    if (dev != cur) (void)hipSetDevice(cur);
+bool same_owner(const FlagSlot *c, int dev, hipStream_t st, pthread_t self) {
+    return c->live && c->dev == dev && c->stream == st && (st != hipStreamPerThread || pthread_equal(c->thread, self));
+}
+
+// queue an array for freeing once the mutex is dropped (caller holds it);
+// with the list full the array is leaked rather than freed under the mutex
+void retire(int dev, int *flags) {
+    if (flags == nullptr || g_nretired >= NRETIRE) return;
+    g_retired[g_nretired++] = Retired{dev, flags};
+}
+
+// free retired arrays with the mutex released: hipFree waits for the device
+// (the kernels and reduces that read them) without blocking other launches
+void free_retired() {
+    Retired r[NRETIRE];
+    int n;
+    {
+        std::lock_guard<std::mutex> g(g_fslot_mu);
+        n = g_nretired;
+        for (int i = 0; i < n; i++) r[i] = g_retired[i];
+        g_nretired = 0;
+    }
+    if (n == 0) return;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (int i = 0; i < n; i++) {
+        if (r[i].dev != cur) (void)hipSetDevice(r[i].dev);
+        (void)hipFree(r[i].flags);
+        if (r[i].dev != cur) (void)hipSetDevice(cur);
+    }
 }
 }  // namespace
 
@@ -176,47 +215,49 @@ Sink sink_acquire(int *status, int sval, hipStream_t st, int64_t nblocks, bool w
     if (!want || nblocks <= 0) return s;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return s;
+    const pthread_t self = pthread_self();
     g_fslot_mu.lock();
     FlagSlot *f = nullptr, *lru = nullptr;
     for (int i = 0; i < NFLAGSLOT; i++) {
         FlagSlot *c = &g_fslot[i];
-        if (c->live && c->dev == dev && c->stream == st) { f = c; break; }
+        if (same_owner(c, dev, st, self)) { f = c; break; }
         if (lru == nullptr || !c->live || (lru->live && c->tick < lru->tick)) lru = c;
     }
     if (f == nullptr) {                 // take a free slot, or the least recently used one
         f = lru;
-        if (f->live) {
-            drain_device(f->dev, dev);          // its last reduce has read the flags
-            if (f->dev != dev) {
-                (void)hipSetDevice(f->dev);
-                (void)hipFree(f->flags);
-                (void)hipSetDevice(dev);
-                f->flags = nullptr;
-                f->cap = 0;
-            }
+        if (f->live) {                  // its last reduce may still be queued: retire the array
+            retire(f->dev, f->flags);
+            f->flags = nullptr;
+            f->cap = 0;
         }
         f->live = true;
         f->dev = dev;
-        f->stream = st;     /* the epoch counter continues: the array may hold old epochs */
+        f->stream = st;
+        f->thread = self;
     }
-    if (f->cap < nblocks) {             // grow: wait for the array's last use on this stream
-        if (f->flags) {
-            (void)hipStreamSynchronize(st);
-            (void)hipFree(f->flags);
-        }
+    if (f->cap < nblocks) {             // grow: the old array may still be read on this stream
+        retire(f->dev, f->flags);
+        f->flags = nullptr;
         f->cap = nblocks > 2 * f->cap ? nblocks : 2 * f->cap;
+    }
+    if (f->flags == nullptr) {
         if (hipMalloc(&f->flags, sizeof(int) * (size_t)f->cap) != hipSuccess ||
             hipMemsetAsync(f->flags, 0, sizeof(int) * (size_t)f->cap, st) != hipSuccess) {
             (void)hipGetLastError();
+            if (f->flags) retire(dev, f->flags);
             f->flags = nullptr;
             f->cap = 0;
+            f->live = false;
             g_fslot_mu.unlock();
+            free_retired();
             return s;                   // per-wave publish
         }
+        f->epoch = 0;                   // a zeroed array: any epoch >= 1 is new to it
     }
     if (++f->epoch >= 0x3fffffff) {     // epochs must not repeat on this array
         if (hipMemsetAsync(f->flags, 0, sizeof(int) * (size_t)f->cap, st) != hipSuccess) {
             g_fslot_mu.unlock();
+            free_retired();
             return s;
         }
         f->epoch = 1;
@@ -228,9 +269,18 @@ Sink sink_acquire(int *status, int sval, hipStream_t st, int64_t nblocks, bool w
 }
 
 static void sink_release(hipStream_t) {
+    const bool pending = g_nretired > 0;
     g_fslot_mu.unlock();
+    if (pending) free_retired();
 }
 
+}  // namespace pncx
+
+namespace pncx {
+int fuse_lanes() {     // read per launch, so tests can run both shapes in one process
+    const char *e = getenv("PNCX_FUSE_LANES");
+    return (e != nullptr && atoi(e) == 1024) ? 1024 : 256;
+}
 }  // namespace pncx
 
 // single status word: any flag of this launch's epoch -> *status = sval

@@ -308,10 +308,17 @@ def batch(segs):
 
 
 # -------------------------------------------------------------- device side
+# the HIP runtime's per-thread stream handle (hip_runtime_api.h: hipStreamPerThread)
+STREAM_PER_THREAD = 2
+
+
 def _stream_ptr(stream):
+    """A torch stream, None (torch's current stream) or a raw hipStream_t value."""
     import torch
     if stream is None:
         stream = torch.cuda.current_stream()
+    if isinstance(stream, int):
+        return ctypes.c_void_p(stream)
     return ctypes.c_void_p(stream.cuda_stream)
 
 

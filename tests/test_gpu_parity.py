@@ -796,15 +796,19 @@ FUSE_CLASSES = [(T.PNCX_PUT, T.NC_SHORT, T.ITYPE_FLOAT), (T.PNCX_GET, T.NC_INT, 
 @pytest.mark.parametrize("cls", FUSE_CLASSES, ids=lambda c: f"{'get' if c[0] == T.PNCX_GET else 'put'}_"
                          f"{T.XNAME[c[1]]}_{T.INAME[c[2]]}")
 @pytest.mark.parametrize("seed", [1, 2])
-def test_dev_batch_fused_two_classes(torch_cuda, cls, seed):
-    """A batch of exactly one conversion class and same-type swaps runs as
-    ONE fused launch (k_batch_fused: four 256-lane conversion tiles per block,
-    then the swap blocks; a class with capped occupancy falls back to two
-    launches).  Random sizes (tile counts not multiples of four, scalar heads
+@pytest.mark.parametrize("lanes", [256, 1024])
+def test_dev_batch_fused_two_classes(torch_cuda, cls, seed, lanes, monkeypatch):
+    """With PNCX_BATCH_FUSE=1 (off by default: no faster) a batch
+    of exactly one conversion class and same-type swaps runs as ONE fused
+    launch (k_batch_fused: 256-lane blocks of one conversion tile or
+    a quarter swap block, or 1024-lane blocks of four tiles or one swap block;
+    a class with capped occupancy falls back to two launches).  Random sizes (tile counts not multiples of four, scalar heads
     and tails), offsets, fills and NC_ERANGE: bit-exact against the oracle,
     synchronous (twice, the second from the plan cache) and asynchronous."""
     torch = torch_cuda
     from pnetcdf_amd import pncx
+    monkeypatch.setenv("PNCX_BATCH_FUSE", "1")
+    monkeypatch.setenv("PNCX_FUSE_LANES", str(lanes))
     ora = OracleConv()
     rng = np.random.default_rng(0xF05E + seed)
     d, xt, it = cls
@@ -865,8 +869,8 @@ def test_dev_batch_fuzz_all_pairs(torch_cuda, seed):
 
 def test_flag_slots_many_streams(torch_cuda):
     """NC_ERANGE flag arrays belong to one (device, stream) and there are 32
-    of them: 40 streams in turn hand slots over (the device is drained
-    first), and a larger launch regrows a slot.  Each call's status and
+    of them: 40 streams in turn hand slots over (the old array is retired and
+    a fresh one zeroed), and a larger launch regrows a slot.  Each call's status and
     bytes must still match the oracle, with the calls of all streams queued
     before anything is read back."""
     torch = torch_cuda
@@ -891,3 +895,48 @@ def test_flag_slots_many_streams(torch_cuda):
         exp, so = ora.putn(5, T.NC_SHORT, vals, T.ITYPE_FLOAT, fill)
         assert int(ds.item()) == so
         assert dx.cpu().numpy().tobytes() == exp
+
+
+def test_flag_slots_stream_per_thread(torch_cuda):
+    """hipStreamPerThread is one handle for a different stream in each host
+    thread, so NC_ERANGE flag arrays are keyed by the calling thread too
+    (ADVICE r2): two threads putting alternately out-of-range and in-range
+    values on their per-thread streams each get their own statuses."""
+    import threading
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    ora = OracleConv()
+    rng = np.random.default_rng(0x7E4D)
+    fill = T.fill_bytes(T.NC_SHORT)
+    n, reps = 1 << 16, 24
+    work = []
+    for t in range(2):
+        items = []
+        for k in range(reps):
+            lo, hi = (-40000.0, 40000.0) if (k + t) % 2 == 0 else (-30000.0, 30000.0)
+            vals = rng.uniform(lo, hi, n).astype(np.float32)
+            items.append((vals, torch.from_numpy(vals).cuda(), torch.zeros(n * 2, dtype=torch.uint8, device="cuda"),
+                          torch.zeros(1, dtype=torch.int32, device="cuda")))
+        work.append(items)
+    torch.cuda.synchronize()
+    errs = []
+
+    def run(items):
+        try:
+            for _vals, di, dx, ds in items:
+                pncx.dev_putn(5, T.NC_SHORT, dx, di, n, T.ITYPE_FLOAT, fill, ds, stream=pncx.STREAM_PER_THREAD)
+        except Exception as e:   # noqa: BLE001 - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(w,)) for w in work]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    torch.cuda.synchronize()
+    assert not errs, errs
+    for items in work:
+        for vals, _di, dx, ds in items:
+            exp, so = ora.putn(5, T.NC_SHORT, vals, T.ITYPE_FLOAT, fill)
+            assert int(ds.item()) == so
+            assert dx.cpu().numpy().tobytes() == exp
