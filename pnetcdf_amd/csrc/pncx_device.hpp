@@ -170,15 +170,25 @@ __device__ __forceinline__ bool in_range(S v, long long lo, unsigned long long h
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool f32_isnan(uint32_t b) { return (b & 0x7fffffffu) > 0x7f800000u; }
 
-// |trunc(x)| for a float with |x| < 2^64 (biased exponent <= 190)
-__device__ __forceinline__ uint64_t f32_trunc_mag(uint32_t b) {
-    const int e = (int)((b >> 23) & 0xffu);
-    const uint32_t m = (b & 0x7fffffu) | 0x800000u;        // x = m * 2^(e - 150)
-    const int sh = e - 150;
-    const uint64_t up = (uint64_t)m << (sh & 63);
-    const int rs = -sh < 31 ? -sh : 31;                      // m < 2^24: >= 24 gives 0
-    const uint32_t dn = m >> (rs & 31);
-    return sh >= 0 ? up : (uint64_t)dn;
+// v_cvt_u32_f32: truncating, saturating, NaN -> 0 (a C cast of an
+// out-of-range float is undefined, so the instruction is named)
+__device__ __forceinline__ uint32_t hw_cvt_u32(float x) {
+    uint32_t r;
+    asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
+// |trunc(x)| for a float with |x| < 2^64 (callers select other inputs away):
+// the two 32-bit halves by exact float arithmetic and two hardware
+// truncating converts -- |x| = hi * 2^32 + lo, where lo keeps a subset of
+// x's 24 significant bits, so the fma is exact.  5 VALU against ~12 for
+// shifting the mantissa by the exponent in 64 bits.  |x| = 2^64 gives
+// hi = 0xffffffff, lo = 0.
+__device__ __forceinline__ uint64_t f32_trunc_mag(float x) {
+    const float xa = __builtin_fabsf(x);
+    const uint32_t hi = hw_cvt_u32(xa * 0x1p-32f);
+    const uint32_t lo = hw_cvt_u32(__builtin_fmaf(-(float)hi, 0x1p32f, xa));
+    return ((uint64_t)hi << 32) | lo;
 }
 
 // x86_cast<T>((double)x) for a float x inside T's checked range or NaN,
@@ -251,24 +261,24 @@ __device__ __forceinline__ typename I<IT>::T get1(typename X<XT>::T xx, bool &ba
         // wave); the same rules: GETF_CheckBND2 for (u)longlong (:518-527),
         // GETF_CheckBND + :511 for long, GETF_CheckBND (:503-513) otherwise
         const uint32_t b = bits_to<uint32_t>(xx);
-        const uint32_t a = b & 0x7fffffffu;
-        const bool nan = f32_isnan(b), neg = (b >> 31) != 0;
+        const bool nan = xx != xx;
         if constexpr (IT == PNCX_ITYPE_LONGLONG || IT == PNCX_ITYPE_LONG) {
             // |x| > 2^63 (not NaN): fill; +-2^63 exactly: INT64_MAX / INT64_MIN;
-            // NaN: cvttsd2si's INT64_MIN
-            const bool o = !nan && a > 0x5f000000u;
-            const uint64_t mag = f32_trunc_mag(b);
-            int64_t r = neg ? -(int64_t)mag : (int64_t)mag;
-            r = a == 0x5f000000u ? (neg ? INT64_MIN : INT64_MAX) : r;
+            // NaN: cvttsd2si's INT64_MIN.  Sign applied as (m ^ s) - s; -2^63
+            // comes out as INT64_MIN by itself, +2^63 is one below it
+            const bool o = __builtin_fabsf(xx) > 0x1p63f;
+            const uint64_t s = (uint64_t)(int64_t)((int32_t)b >> 31);
+            int64_t r = (int64_t)((f32_trunc_mag(xx) ^ s) - s);
+            r = b == 0x5f000000u ? INT64_MAX : r;
             r = nan ? INT64_MIN : r;
             bad |= o;
             return o ? II::fill() : r;
         } else if constexpr (IT == PNCX_ITYPE_ULONGLONG) {
             // x > 2^64 or x < 0 (not -0, not NaN): fill; 2^64 exactly:
-            // UINT64_MAX; NaN: 2^63 (cvtt_u64)
-            const bool o = !nan && (a > 0x5f800000u || (neg && a != 0));
-            uint64_t r = f32_trunc_mag(b);
-            r = a == 0x5f800000u ? UINT64_MAX : r;
+            // UINT64_MAX (hi is already all ones); NaN: 2^63 (cvtt_u64)
+            const bool o = xx > 0x1p64f || xx < 0.0f;
+            uint64_t r = f32_trunc_mag(xx);
+            r = b == 0x5f800000u ? UINT64_MAX : r;
             r = nan ? 0x8000000000000000ull : r;
             bad |= o;
             return o ? II::fill() : r;
@@ -327,16 +337,17 @@ __device__ __forceinline__ typename X<XT>::T put1(typename I<IT>::T v, typename 
         XT_T r;
         if constexpr (XT == NC_INT64 || XT == NC_UINT64) {
             const uint32_t b = bits_to<uint32_t>(v);
-            const uint32_t a = b & 0x7fffffffu;
-            const uint64_t mag = f32_trunc_mag(b);
+            const uint64_t mag = f32_trunc_mag(v);
             if constexpr (XT == NC_INT64) {
-                // 2^63 (either sign) and NaN: cvttsd2si's INT64_MIN
-                const int64_t sv = (b >> 31) ? -(int64_t)mag : (int64_t)mag;
-                r = a >= 0x5f000000u ? INT64_MIN : sv;
+                // |x| >= 2^63 and NaN: cvttsd2si's INT64_MIN (the larger ones
+                // are out of range: fill below)
+                const uint64_t s = (uint64_t)(int64_t)((int32_t)b >> 31);
+                const int64_t sv = (int64_t)((mag ^ s) - s);
+                r = !(__builtin_fabsf(v) < 0x1p63f) ? INT64_MIN : sv;
             } else {
                 // cvtt_u64: 2^64 -> 0, NaN -> 2^63, [0, 2^64) exact
-                uint64_t u = a == 0x5f800000u ? 0ull : mag;
-                r = f32_isnan(b) ? 0x8000000000000000ull : u;
+                uint64_t u = b == 0x5f800000u ? 0ull : mag;
+                r = v != v ? 0x8000000000000000ull : u;
             }
         } else {
             r = f32_cast<XT_T>(v);

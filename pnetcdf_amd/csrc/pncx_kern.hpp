@@ -476,6 +476,15 @@ struct Shape {
     static constexpr int TILE = LANES * E;                // elements per block tile
     static constexpr int E2 = 16 / W;                     // elements per wide 16 B chunk
     static constexpr int LDS_BYTES = USE_LDS ? 16 * LANES : 16;
+    // tiles per block of the direct shapes (k_tile_u): the 2:1 widening
+    // tiles with a range test or from 1-byte elements keep two loads per
+    // lane in flight through their conversion -- float -> (u)int64 73.0-76.3
+    // -> 80.3-81.4 %, NC_BYTE -> short 78.5 -> 82.0 %, every 1:2 pair +1.2
+    // to +3.5 points, short -> uint +1.7 -- while plain widening casts are
+    // level or lose (NC_INT -> double, C3: 82.7 -> 82.0 % in the bench) and
+    // the 1:1 tiles lose 2-10 points with two (tools/gpu_tile_u.sh,
+    // profiles/r03k_matrix_u{1,2}.jsonl, profiles/r03l_c3_tile_u.txt)
+    static constexpr int TILE_U = !USE_LDS && SS < DS && (SS == 1 || may_range<Op>::value) ? 2 : 1;
     // dynamic LDS requested at launch on top of the static tile
     static constexpr int PAD_LDS = OCC_LDS > LDS_BYTES ? OCC_LDS - LDS_BYTES : 0;
 };
@@ -613,6 +622,52 @@ __global__ __launch_bounds__(Shape<Op>::LANES) void k_tile(const uint8_t *src, u
     }
     publish(sk, sk.status, bad);
 }
+
+// Direct-shape ops with U tiles per block (Shape::TILE_U): all U loads of a
+// lane issued before its first convert, so a wave keeps U vectors in flight
+// through a long conversion.  The loads are unpredicated (a lane past the
+// last tile re-reads it), the stores predicated.
+template <class Op, bool NT, int U>
+__global__ __launch_bounds__(Shape<Op>::LANES) void k_tile_u(const uint8_t *src, uint8_t *dst, int64_t head,
+                                                             int64_t ntile, int64_t n, typename Op::fill_t fill,
+                                                             Sink sk) {
+    using S = Shape<Op>;
+    static_assert(!S::USE_LDS, "direct shapes only");
+    constexpr int SS = S::SS, DS = S::DS, E = S::E, SB = E * SS, DB = E * DS;
+    bool bad = false;
+    const int64_t nb = gridDim.x;
+    if (blockIdx.x == 0) {
+        scalar_range<Op, S::LANES>(src, dst, 0, head, fill, bad);
+        scalar_range<Op, S::LANES>(src, dst, head + ntile * S::TILE, n, fill, bad);
+    }
+    const uint8_t *ts = src + head * SS;
+    uint8_t *td = dst + head * DS;
+    const int64_t ngroup = (ntile + U - 1) / U;
+    for (int64_t g = xcd_remap(blockIdx.x, nb); g < ngroup; g += nb) {
+        typename VecT<SB>::type v[U];
+#pragma unroll
+        for (int i = 0; i < U; i++) {
+            const int64_t t0 = g * U + i, t = t0 < ntile ? t0 : ntile - 1;    // unpredicated, clamped
+            v[i] = ldv<SB, NT>(ts + (t * (int64_t)S::TILE + threadIdx.x * E) * SS);
+        }
+#pragma unroll
+        for (int i = 0; i < U; i++) {
+            const int64_t t = g * U + i;
+            if (t < ntile) {
+                alignas(16) uint8_t sb[SB];
+                alignas(16) uint8_t db[DB];
+                __builtin_memcpy(sb, &v[i], SB);
+                conv_regs<Op, E>(sb, db, fill, bad);
+                typename VecT<DB>::type o;
+                __builtin_memcpy(&o, db, DB);
+                stv<DB, NT>(td + (t * (int64_t)S::TILE + threadIdx.x * E) * DS, o);
+            }
+        }
+    }
+    publish(sk, sk.status, bad);
+}
+
+int tile_u(int dflt);   // PNCX_TILE_U = 1 / 2 / 4 overrides the op's TILE_U (A/B)
 
 // fully scalar (misaligned buffers): one element per lane, byte-wise access
 template <class Op>
@@ -1247,9 +1302,22 @@ int launch_stream(const pncxk_args *a) {
                            nvec, n, fill, sk);
     } else {
         const int64_t ntile = (n - h) / Shape<Op>::TILE;
-        grid = ntile < 1 ? 1 : ntile;
+        const int u = Shape<Op>::USE_LDS ? 1 : tile_u(Shape<Op>::TILE_U);
+        grid = ntile < 1 ? 1 : (ntile + u - 1) / u;
         if (grid > MAX_BLOCKS) grid = MAX_BLOCKS;
         sk = sink_acquire(a->status, NC_ERANGE, st, grid, want);
+        if constexpr (!Shape<Op>::USE_LDS) {
+            if (u == 2 && a->nontemporal >= 0) {
+                hipLaunchKernelGGL((k_tile_u<Op, true, 2>), dim3((unsigned)grid), dim3(Shape<Op>::LANES), 0, st, src,
+                                   dst, h, ntile, n, fill, sk);
+                return sink_finish(sk, st, grid, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
+            }
+            if (u == 4 && a->nontemporal >= 0) {
+                hipLaunchKernelGGL((k_tile_u<Op, true, 4>), dim3((unsigned)grid), dim3(Shape<Op>::LANES), 0, st, src,
+                                   dst, h, ntile, n, fill, sk);
+                return sink_finish(sk, st, grid, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
+            }
+        }
         if (a->nontemporal >= 0)
             hipLaunchKernelGGL((k_tile<Op, true>), dim3((unsigned)grid), dim3(Shape<Op>::LANES), Shape<Op>::PAD_LDS, st,
                                src, dst, h, ntile, n, fill, sk);

@@ -277,6 +277,12 @@ static void sink_release(hipStream_t) {
 }  // namespace pncx
 
 namespace pncx {
+int tile_u(int dflt) {     // read per launch: tests run both shapes in one process
+    const char *e = getenv("PNCX_TILE_U");
+    const int v = e != nullptr ? atoi(e) : dflt;
+    return v == 1 || v == 2 || v == 4 ? v : dflt;
+}
+
 int fuse_lanes() {     // read per launch, so tests can run both shapes in one process
     const char *e = getenv("PNCX_FUSE_LANES");
     return (e != nullptr && atoi(e) == 1024) ? 1024 : 256;

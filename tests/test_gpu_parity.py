@@ -89,6 +89,28 @@ def test_random_bits_vs_oracle(conv, xt):
             assert sg == so and g.tobytes() == o.tobytes(), (T.INAME[it], n)
 
 
+@pytest.mark.parametrize("u", [1, 2, 4])
+def test_tiles_per_block_vs_oracle(torch_cuda, u, monkeypatch):
+    """The direct-shape kernels with 1, 2 or 4 tiles per block (k_tile /
+    k_tile_u, PNCX_TILE_U; the default is 2 for the 2:1 widening tiles and 1
+    otherwise): every pair both ways on random bits, with tile counts that
+    are not multiples of u and scalar tails."""
+    monkeypatch.setenv("PNCX_TILE_U", str(u))
+    dev, ora = HipDevConv(), OracleConv()
+    rng = np.random.default_rng(0x711E + u)
+    for xt in T.NUMERIC_XTYPES:
+        for it in T.NUMERIC_ITYPES:
+            for n in (4099, 100003):
+                raw = rng.integers(0, 256, n * 8, dtype=np.uint8)
+                ib = np.frombuffer(raw.tobytes(), T.ITYPE_NP[it])[:n].copy()
+                fill = T.fill_bytes(xt, 77)
+                assert dev.putn(5, xt, ib, it, fill) == ora.putn(5, xt, ib, it, fill), (T.INAME[it], n)
+                xr = rng.integers(0, 256, n * T.xlen(xt), dtype=np.uint8).tobytes()
+                g, sg = dev.getn(5, xt, xr, it)
+                o, so = ora.getn(5, xt, xr, it)
+                assert sg == so and g.tobytes() == o.tobytes(), (T.XNAME[xt], T.INAME[it], n)
+
+
 # ------------------------------------- the reference's own test expectations
 @pytest.mark.parametrize("cdf", [2, 5])
 def test_reference_nc_test(conv, cdf):

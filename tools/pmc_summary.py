@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # C2 32 GiB of NC_DOUBLE, C3 2^31 NC_INT, C4 256 x 2^20)
 WORKLOADS = {
     "c2": ("swap8", [r"k_tile<pncx::SwapOp<8>"], 16, 1 << 32),
-    "c3": ("get_int_double", [r"k_tile<pncx::GetOp<4, 9>"], 12, 1 << 31),
+    "c3": ("get_int_double", [r"k_tile(_u)?<pncx::GetOp<4, 9>"], 12, 1 << 31),
     "c4": ("batch_c4", [r"k_batch_swapmix"], 6, 1 << 28),
     "c4_erange": ("batch_c4_erange", [r"k_batch<pncx::PutOp<3, 8, false>", r"k_batch_swapmix"], 7, 1 << 28),
 }
