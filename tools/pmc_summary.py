@@ -1,6 +1,6 @@
 """Summarise rocprofv3 output into profiles/ (kernel stats + HBM traffic).
 
-    python tools/pmc_summary.py <prof_dir> <round_tag>
+    python tools/pmc_summary.py <prof_dir> <round_tag> [out_dir]
 
 Reads <prof_dir>/trace/*_kernel_stats.csv and the FETCH_SIZE / WRITE_SIZE
 counter_collection CSVs of tools/gpu_profile.sh (one counter per pass, one
@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # C2 32 GiB of NC_DOUBLE, C3 2^31 NC_INT, C4 256 x 2^20)
 WORKLOADS = {
     "c2": ("swap8", [r"k_tile<pncx::SwapOp<8>"], 16, 1 << 32),
-    "c3": ("get_int_double", [r"k_tile(_u)?<pncx::GetOp<4, 9>"], 12, 1 << 31),
+    "c3": ("get_int_double", [r"k_tile<pncx::GetOp<4, 9>"], 12, 1 << 31),
     "c4": ("batch_c4", [r"k_batch_swapmix"], 6, 1 << 28),
     "c4_erange": ("batch_c4_erange", [r"k_batch<pncx::PutOp<3, 8, false>", r"k_batch_swapmix"], 7, 1 << 28),
 }
@@ -58,7 +58,7 @@ def counter(prof, ctr, w, pats):
 
 def main():
     prof, tag = sys.argv[1], sys.argv[2]
-    out_dir = os.path.join(ROOT, "profiles")
+    out_dir = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "profiles")
     os.makedirs(out_dir, exist_ok=True)
     for p in glob.glob(os.path.join(prof, "trace", "**", "*_kernel_stats.csv"), recursive=True):
         shutil.copy(p, os.path.join(out_dir, f"{tag}_{os.path.basename(p)}"))
