@@ -977,8 +977,9 @@ __global__ __launch_bounds__(256) void k_tmap_runs(const uint8_t *src, uint8_t *
 constexpr int XT_P = 64, XT_U = 128;
 
 struct TransposeGeom {
-    int64_t cp, cu;          // count[P], count[U]
+    int64_t cp, cu;          // count[P] (merged: count[P-1] * count[P]), count[U]
     int64_t ip, iu;          // imap[P], imap[U] (user elements)
+    int64_t cin, ip2;        // merged P: count[P], imap[P-1] (virtual row f = (f / cin, f % cin))
     int64_t su;              // packed stride of U
     int64_t tp, tu;          // tiles along P and U
     int64_t ntiles;          // tp * tu * outer
@@ -1003,7 +1004,46 @@ __device__ __forceinline__ void st_nt(uint8_t *p, T v) {
 // indices are clamped into the tile, so the extra lanes re-read (and
 // convert) valid elements and only the stores are predicated -- a predicated
 // load costs a wait of its own (5.0 -> 4.0 TB/s measured).
-template <class Op, bool GATHER, bool FULL, typename TU, bool SC1>
+// user-side element offset of (virtual) tile row f: f * imap[P], or with the
+// last two dimensions merged (MRG) (f / count[P]) * imap[P-1] + (f % count[P]) * imap[P]
+template <bool MRG>
+__device__ __forceinline__ int64_t xrow(const TransposeGeom &g, int64_t f) {
+    if constexpr (MRG) {
+        const uint64_t q = (uint64_t)f / (uint64_t)g.cin;
+        return (int64_t)q * g.ip2 + (f - (int64_t)q * g.cin) * g.ip;
+    } else {
+        return f * g.ip;
+    }
+}
+
+// a lane's running user-row pointer over rows f, f + RPP, f + 2 RPP, ...: with
+// MRG the inner index wraps at count[P] (count[P] >= 16 > RPP: one wrap per step)
+template <bool MRG, int RPP>
+struct XRows {
+    const uint8_t *ptr;
+    int64_t p, step, wrap, cin;
+    __device__ __forceinline__ XRows(const uint8_t *row0, const TransposeGeom &g, int64_t f, int64_t es) {
+        ptr = row0 + xrow<MRG>(g, f) * es;
+        step = RPP * g.ip * es;
+        if constexpr (MRG) {
+            cin = g.cin;
+            p = f % g.cin;
+            wrap = (g.ip2 - g.cin * g.ip) * es;
+        }
+    }
+    __device__ __forceinline__ void next() {
+        ptr += step;
+        if constexpr (MRG) {
+            p += RPP;
+            if (p >= cin) {
+                p -= cin;
+                ptr += wrap;
+            }
+        }
+    }
+};
+
+template <class Op, bool GATHER, bool FULL, typename TU, bool SC1, bool MRG = false>
 __device__ __forceinline__ void xpose_tile(const uint8_t *src, uint8_t *dst, const TransposeGeom &g, int64_t pbase,
                                            int64_t ubase, int64_t p0, int64_t u0, int np, int nu,
                                            TU (*tile)[XT_U + 1], typename Op::fill_t fill, bool &bad) {
@@ -1015,22 +1055,22 @@ __device__ __forceinline__ void xpose_tile(const uint8_t *src, uint8_t *dst, con
     constexpr int CPP = 256 / XT_P, NC = XT_U / CPP;      // packed side: columns per pass, passes
     const int lu = threadIdx.x % XT_U, ru = threadIdx.x / XT_U;     // user-side lane, row
     const int lp = threadIdx.x % XT_P, cp = threadIdx.x / XT_P;     // packed-side lane, column
-    const int64_t rs = g.ip * UES, cs = g.su * PES;        // bytes between rows p (user), columns u (packed)
+    const int64_t cs = g.su * PES;                         // bytes between columns u (packed)
     if constexpr (GATHER) {
         const int cl = FULL || lu < nu ? lu : nu - 1;
-        const uint8_t *s0 = src + (ubase + p0 * g.ip + (u0 + cl) * g.iu) * UES;
+        const uint8_t *s0 = src + (ubase + (u0 + cl) * g.iu) * UES;      // column cl of row 0
         TU v[NR];
         if constexpr (FULL) {
             // one running address: 32 precomputed 64-bit addresses would cost
             // 64 VGPRs on top of the 64 the data takes
-            const uint8_t *sp = s0 + ru * rs;
+            XRows<MRG, RPP> sp(s0, g, p0 + ru, UES);
 #pragma unroll
-            for (int i = 0; i < NR; i++, sp += RPP * rs) v[i] = ld_nt<TU>(sp);
+            for (int i = 0; i < NR; i++, sp.next()) v[i] = ld_nt<TU>(sp.ptr);
         } else {
 #pragma unroll
             for (int i = 0; i < NR; i++) {
                 const int r = ru + RPP * i < np ? ru + RPP * i : np - 1;
-                v[i] = ld_nt<TU>(s0 + r * rs);
+                v[i] = ld_nt<TU>(s0 + xrow<MRG>(g, p0 + r) * UES);
             }
         }
 #pragma unroll
@@ -1073,18 +1113,18 @@ __device__ __forceinline__ void xpose_tile(const uint8_t *src, uint8_t *dst, con
 #pragma unroll
         for (int i = 0; i < NC; i++) tile[lp][cp + CPP * i] = Op::one(v[i], DU(0), fill, bad);
         __syncthreads();
-        uint8_t *d0 = dst + (ubase + p0 * g.ip + (u0 + lu) * g.iu) * UES;
+        uint8_t *d0 = dst + (ubase + (u0 + lu) * g.iu) * UES;             // column lu of row 0
         TU o[NR];
 #pragma unroll
         for (int i = 0; i < NR; i++) o[i] = tile[ru + RPP * i][lu];
         if constexpr (FULL) {
-            uint8_t *dp = d0 + ru * rs;
+            XRows<MRG, RPP> dp(d0, g, p0 + ru, UES);
 #pragma unroll
-            for (int i = 0; i < NR; i++, dp += RPP * rs) st_nt<TU, SC1>(dp, o[i]);
+            for (int i = 0; i < NR; i++, dp.next()) st_nt<TU, SC1>(const_cast<uint8_t *>(dp.ptr), o[i]);
         } else {
 #pragma unroll
             for (int i = 0; i < NR; i++)
-                if (ru + RPP * i < np && lu < nu) st_nt<TU, SC1>(d0 + (ru + RPP * i) * rs, o[i]);
+                if (ru + RPP * i < np && lu < nu) st_nt<TU, SC1>(d0 + xrow<MRG>(g, p0 + ru + RPP * i) * UES, o[i]);
         }
     }
 }
@@ -1097,7 +1137,7 @@ __device__ __forceinline__ void xpose_tile(const uint8_t *src, uint8_t *dst, con
 // SC1 = false: plain nontemporal stores -- unlike the streaming sweeps, the
 // transpose runs 2 points faster without write-through (65.9 against 63.7 %
 // of peak, profiles/r02_transpose_sweep_product.txt)
-template <class Op, bool GATHER, bool ALIGNED, bool SC1 = false>
+template <class Op, bool GATHER, bool ALIGNED, bool SC1 = false, bool MRG = false>
 __global__ __launch_bounds__(256, 2) void k_imap_tile(const uint8_t *src, uint8_t *dst, TransposeGeom g,
                                                    typename Op::fill_t fill, Sink sk) {
     using SU = typename Op::SU;
@@ -1142,9 +1182,9 @@ __global__ __launch_bounds__(256, 2) void k_imap_tile(const uint8_t *src, uint8_
         const int np = (int)(g.cp - p0 < XT_P ? g.cp - p0 : XT_P), nu = (int)(g.cu - u0 < XT_U ? g.cu - u0 : XT_U);
         if (ALIGNED) {
             if (np == XT_P && nu == XT_U)
-                xpose_tile<Op, GATHER, true, TU, SC1>(src, dst, g, pbase, ubase, p0, u0, np, nu, tile, fill, bad);
+                xpose_tile<Op, GATHER, true, TU, SC1, MRG>(src, dst, g, pbase, ubase, p0, u0, np, nu, tile, fill, bad);
             else
-                xpose_tile<Op, GATHER, false, TU, SC1>(src, dst, g, pbase, ubase, p0, u0, np, nu, tile, fill, bad);
+                xpose_tile<Op, GATHER, false, TU, SC1, MRG>(src, dst, g, pbase, ubase, p0, u0, np, nu, tile, fill, bad);
         } else if (GATHER) {
             // user -> LDS, lanes along U
             for (int r = ru; r < np; r += RPP)
@@ -1175,10 +1215,21 @@ __global__ __launch_bounds__(256, 2) void k_imap_tile(const uint8_t *src, uint8_
     publish(sk, sk.status, bad);
 }
 
+int xpose_merge();   // PNCX_XPOSE_MERGE=0 tiles P alone (A/B); default 1
+
 // Pick the transpose kernel for a varm layout: P = last dim, U = the other
 // dim with the smallest imap; worth it when P is strided in the user buffer
 // and U is (nearly) contiguous there.
-inline bool transpose_geom(const pncxk_imap *m, TransposeGeom *g) {
+// merge: when U is not P-1, tile P-1 and P as one virtual dimension of
+// count[P-1] * count[P] rows.  For fixed u the packed bytes of (P-1, P) are
+// one contiguous run, so 64-row tiles of it start on 512-byte boundaries of
+// that run, and no cache line of the packed buffer is written by two blocks
+// when the run's length is a multiple of 128 bytes.  Tiling P alone, a
+// packed row of count[P] elements that is not a multiple of 128 bytes splits
+// a line between neighbouring tiles at every tile edge: 1024 x 1024 x 250
+// doubles (2000-byte rows) ran at 46 % of peak against 68 % for x 256, and
+// x 254 at 31 % (tools/transpose_probe.py, profiles/r03n_xpose_shapes.jsonl).
+inline bool transpose_geom(const pncxk_imap *m, TransposeGeom *g, bool merge) {
     const int nd = m->ndims, P = nd - 1;
     int U = -1;
     if (m->tmode != 0 || nd < 2) return false;
@@ -1189,17 +1240,20 @@ inline bool transpose_geom(const pncxk_imap *m, TransposeGeom *g) {
     int64_t pst[PNCX_MAX_DIMS];
     int64_t s = 1;
     for (int d = nd - 1; d >= 0; d--) { pst[d] = s; s *= m->count[d]; }
-    g->cp = m->count[P];
+    const bool mrg = merge && U < P - 1 && m->count[P - 1] > 1;
+    g->cp = mrg ? m->count[P - 1] * m->count[P] : m->count[P];
     g->cu = m->count[U];
     g->ip = m->imap[P];
     g->iu = m->imap[U];
+    g->cin = mrg ? m->count[P] : 0;
+    g->ip2 = mrg ? m->imap[P - 1] : 0;
     g->su = pst[U];
     g->tp = (g->cp + XT_P - 1) / XT_P;
     g->tu = (g->cu + XT_U - 1) / XT_U;
     g->nod = 0;
     int64_t outer = 1;
     for (int d = 0; d < P; d++) {
-        if (d == U) continue;
+        if (d == U || (mrg && d == P - 1)) continue;
         g->ocount[g->nod] = m->count[d];
         g->ostride_p[g->nod] = pst[d];
         g->ostride_u[g->nod] = m->imap[d];
@@ -1231,17 +1285,20 @@ int launch_imap(const pncxk_args *a, const pncxk_imap *m, int gather) {
         else hipLaunchKernelGGL((k_tmap_runs<Op, false>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, sk);
         return sink_finish(sk, st, grid, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
     }
-    if (transpose_geom(m, &g)) {
+    const int ues = gather ? Op::SS : Op::DS, pes = gather ? Op::DS : Op::SS;
+    const bool al = (uintptr_t)src % (uintptr_t)(gather ? ues : pes) == 0 &&
+                    (uintptr_t)dst % (uintptr_t)(gather ? pes : ues) == 0;
+    if (transpose_geom(m, &g, al && xpose_merge())) {       // the loops (unaligned) tile P alone
         const unsigned grid = (unsigned)(g.ntiles < MAX_BLOCKS ? g.ntiles : MAX_BLOCKS);
-        const int ues = gather ? Op::SS : Op::DS, pes = gather ? Op::DS : Op::SS;
-        const bool al = (uintptr_t)src % (uintptr_t)(gather ? ues : pes) == 0 &&
-                        (uintptr_t)dst % (uintptr_t)(gather ? pes : ues) == 0;
+        const bool mrg = g.cin > 0;
         const Sink sk = sink_acquire(a->status, NC_ERANGE, st, grid, want);
         if (gather) {
-            if (al) hipLaunchKernelGGL((k_imap_tile<Op, true, true>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, sk);
+            if (al && mrg) hipLaunchKernelGGL((k_imap_tile<Op, true, true, false, true>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, sk);
+            else if (al) hipLaunchKernelGGL((k_imap_tile<Op, true, true>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, sk);
             else hipLaunchKernelGGL((k_imap_tile<Op, true, false>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, sk);
         } else {
-            if (al) hipLaunchKernelGGL((k_imap_tile<Op, false, true>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, sk);
+            if (al && mrg) hipLaunchKernelGGL((k_imap_tile<Op, false, true, false, true>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, sk);
+            else if (al) hipLaunchKernelGGL((k_imap_tile<Op, false, true>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, sk);
             else hipLaunchKernelGGL((k_imap_tile<Op, false, false>), dim3(grid), dim3(256), 0, st, src, dst, g, fill, sk);
         }
         return sink_finish(sk, st, grid, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);

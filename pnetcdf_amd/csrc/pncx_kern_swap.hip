@@ -283,6 +283,11 @@ int tile_u(int dflt) {     // read per launch: tests run both shapes in one proc
     return v == 1 || v == 2 || v == 4 ? v : dflt;
 }
 
+int xpose_merge() {     // read per launch: tests run both tilings in one process
+    const char *e = getenv("PNCX_XPOSE_MERGE");
+    return e == nullptr || atoi(e) != 0;
+}
+
 int fuse_lanes() {     // read per launch, so tests can run both shapes in one process
     const char *e = getenv("PNCX_FUSE_LANES");
     return (e != nullptr && atoi(e) == 1024) ? 1024 : 256;

@@ -146,3 +146,27 @@ def test_imap_tile_alignment(torch_cuda, xt, it, ushift, xshift):
     torch.cuda.synchronize()
     assert int(ds.item()) == gst
     assert ubuf.cpu().numpy()[ushift:ushift + span * isz].tobytes() == exp_user.view(np.uint8).tobytes()
+
+
+# the transposes whose last two dimensions are tiled as one (U is not P-1):
+# 2000-byte packed rows, a 4-D request with an outer dim between U and
+# (P-1, P), count[P] = 16 (the smallest: a lane's two-row step wraps), a
+# padded U (imap 2), and partial tiles at the end of the merged rows
+MERGE_CASES = [
+    ([130, 9, 250], [1, 130, 1170]),
+    ([130, 5, 7, 70], [1, 130, 650, 4550]),
+    ([150, 33, 16], [1, 150, 4950]),
+    ([65, 11, 37], [2, 130, 1430]),
+    ([129, 3, 19], [1, 129, 387]),
+]
+
+
+@pytest.mark.parametrize("count,imap", MERGE_CASES)
+@pytest.mark.parametrize("xt,it", [(T.NC_INT, T.ITYPE_DOUBLE), (T.NC_DOUBLE, T.ITYPE_DOUBLE), (T.NC_UINT64, T.ITYPE_SCHAR)])
+@pytest.mark.parametrize("merge", ["1", "0"])
+def test_imap_tile_merged_dims(torch_cuda, count, imap, xt, it, merge, monkeypatch):
+    """k_imap_tile with the last two dimensions tiled as one virtual row
+    (default) and tiled P alone (PNCX_XPOSE_MERGE=0): put and get against a
+    numpy gather/scatter + the oracle, on device buffers."""
+    monkeypatch.setenv("PNCX_XPOSE_MERGE", merge)
+    test_imap_put_get(torch_cuda, count, imap, xt, it, "dev")
