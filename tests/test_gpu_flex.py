@@ -248,3 +248,17 @@ def test_flex_mpi_file_parity(tmp_path):
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     assert "file: 0 failure(s)" in r.stdout
     assert r.stdout.count("ok file") == 4 * 14
+
+
+@pytest.mark.parametrize("xt,it", [(T.NC_DOUBLE, T.ITYPE_DOUBLE), (T.NC_SHORT, T.ITYPE_INT)])
+def test_flex_short_runs_many_steps(torch_cuda, xt, it):
+    """the 16-bit-map short-run path with 2^17 runs x 12 copies: every lane
+    takes several grid-stride steps and the last one is ragged"""
+    rng = np.random.default_rng(0x70FF)
+    nb = 1 << 17
+    blen = rng.integers(1, 8, nb)
+    gaps = rng.integers(0, 5, nb)
+    disp = np.concatenate([[0], np.cumsum(blen + gaps)[:-1]]).astype(np.int64)
+    dt = run_case(torch_cuda, "dev", xt, it, disp.tolist(), blen.tolist(), int(disp[-1] + blen[-1] + 2), 12,
+                  None, None, 31)
+    assert dt.inq()["layout"] == 2
