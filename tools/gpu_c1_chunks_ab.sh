@@ -2,6 +2,7 @@
 # on /dev/shm, host buffers) by pipeline chunk count (PNCX_MIN_CHUNKS) and
 # I/O threads, alternating; the file-layer GPU tests first.
 #   bash tools/gpu_c1_chunks_ab.sh <tag> [rounds]
+# (PNCX_MIN_CHUNKS existed only in the A/B build; the product keeps one chunk per slot.)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/c1_ab_$1

@@ -2,6 +2,7 @@
 # 1024 (product) / 512 / 256) on C4, synchronous and asynchronous calls,
 # alternating runs on one box; parity of the batch tests at 256 first.
 #   bash tools/gpu_mix_lanes_ab.sh <tag> [rounds]
+# (PNCX_MIX_BLOCK_LANES existed only in the A/B build; the product keeps 1024.)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/mix_ab_$1
