@@ -441,7 +441,10 @@ static int host_staged(const op_t *op, const void *src, void *dst, long long n, 
     ctx_t *c = get_ctx();
     size_t per_elem, chunk_elems, cb;
     long long off;
-    int slot, err = 0, st0 = 0, st1 = 0, i;
+    int slot, err = 0, st[NSLOT] = {0}, i, used;
+    /* a same-type swap cannot report NC_ERANGE: no status words to zero or
+     * read back (each costs a command and, for the read, a synchronise) */
+    const int want_status = op->kind != PNCXK_SWAP;
     pinned_t pn = {{NULL, NULL}, 0};
     if (c == NULL) return PNCX_EDEVICE;
     pthread_mutex_lock(&c->lock);
@@ -453,7 +456,8 @@ static int host_staged(const op_t *op, const void *src, void *dst, long long n, 
     if (chunk_elems < 1) chunk_elems = 1;
     if ((long long)chunk_elems > n) chunk_elems = (size_t)n;
     err = ensure_dbuf(c, ALIGN16(chunk_elems * op->ss) + ALIGN16(chunk_elems * op->ds));
-    for (i = 0; i < NSLOT && !err; i++)
+    used = (long long)chunk_elems >= n ? 1 : NSLOT;            /* slots (streams) this call touches */
+    for (i = 0; i < used && want_status && !err; i++)
         err = pncxrt_memset(c->dstatus + i, 0, sizeof(int), c->stream[i]);
     for (off = 0, slot = 0; off < n && !err; off += (long long)chunk_elems, slot ^= 1) {
         long long m = n - off < (long long)chunk_elems ? n - off : (long long)chunk_elems;
@@ -467,21 +471,23 @@ static int host_staged(const op_t *op, const void *src, void *dst, long long n, 
         if (!err && preserve && dout != din) err = pncxrt_memcpy_h2d(dout, hd, (size_t)m * op->ds, s);
         if (!err) {
             if (!(op->kind == PNCXK_SWAP && op->a == 1 && dout == din))
-                err = launch_op(op, din, dout, m, c->dstatus + slot, s);
+                err = launch_op(op, din, dout, m, want_status ? c->dstatus + slot : NULL, s);
         }
         if (!err) err = pncxrt_memcpy_d2h(hd, dout, (size_t)m * op->ds, s);
     }
-    for (i = 0; i < NSLOT; i++) {
+    for (i = 0; i < used; i++) {
         int e2 = pncxrt_stream_sync(c->stream[i]);
         if (!err && e2) err = e2;
     }
-    if (!err) err = pncxrt_memcpy_d2h(&st0, c->dstatus, sizeof(int), c->stream[0]);
-    if (!err) err = pncxrt_memcpy_d2h(&st1, c->dstatus + 1, sizeof(int), c->stream[0]);
-    if (!err) err = pncxrt_stream_sync(c->stream[0]);
+    /* both streams are done: the used status words in one copy */
+    if (!err && want_status) err = pncxrt_memcpy_d2h(st, c->dstatus, sizeof(int) * (size_t)used, c->stream[0]);
+    if (!err && want_status) err = pncxrt_stream_sync(c->stream[0]);
     unpin_all(&pn);
     pthread_mutex_unlock(&c->lock);
     if (err) return err < 0 ? err : PNCX_EDEVICE;
-    return st0 != 0 ? st0 : st1;
+    for (i = 0; i < used; i++)
+        if (st[i] != 0) return st[i];
+    return NC_NOERR;
 }
 
 /* ------------------------------------------------------------------------ */
