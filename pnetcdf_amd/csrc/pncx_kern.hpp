@@ -918,6 +918,41 @@ __global__ __launch_bounds__(256) void k_imap(const uint8_t *src, uint8_t *dst, 
     publish(sk, sk.status, bad);
 }
 
+// Uniform runs (tmode 1, the MPI vector / strided types) over a contiguous
+// count, when every run holds whole 16-byte vectors: a lane moves one vector
+// of E = 16 / (wider element size) elements, which never straddles a run or
+// a copy, with one run division per vector instead of per element, and 16
+// bytes per lane on the wider side (k_imap moves one element per lane).
+// One vector per lane, one-shot grid, XCD order, as k_tile.
+template <class Op, bool GATHER>
+__global__ __launch_bounds__(256) void k_urun(const uint8_t *src, uint8_t *dst, int64_t nvec, pncxk_imap m,
+                                              typename Op::fill_t fill, Sink sk) {
+    constexpr int SS = Op::SS, DS = Op::DS, W = SS > DS ? SS : DS, E = 16 / W;
+    constexpr int SB = E * SS, DB = E * DS, UES = GATHER ? SS : DS;
+    bool bad = false;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const uint32_t tn = (uint32_t)m.tn, tlen = (uint32_t)m.tlen;
+    for (int64_t v = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 + threadIdx.x; v < nvec; v += stride) {
+        const int64_t k = v * E;                              // first packed element of the vector
+        const int64_t c = k / tn;
+        const uint32_t r = (uint32_t)(k - c * tn), q = r / tlen, e = r - q * tlen;
+        const int64_t ub = c * m.textent + m.tdisp0 + (int64_t)q * m.tstride + (int64_t)e * UES;
+        const uint8_t *ps = GATHER ? src + ub : src + k * SS;
+        uint8_t *pd = GATHER ? dst + k * DS : dst + ub;
+        alignas(16) uint8_t sb[SB];
+        alignas(16) uint8_t db[DB];
+        const auto x = ldv<SB, true>(ps);
+        __builtin_memcpy(sb, &x, SB);
+        conv_regs<Op, E>(sb, db, fill, bad);
+        typename VecT<DB>::type o;
+        __builtin_memcpy(&o, db, DB);
+        stv<DB, true>(pd, o);
+    }
+    publish(sk, sk.status, bad);
+}
+
+int urun_enabled();   // PNCX_URUN (default 1)
+
 // Derived buftype in packed order with long runs (tmode 3, or uniform runs
 // of 256..4096 elements, tmode 1): one wave per run
 // piece (pieces of at most PNCX_TMAP_PIECE elements, split at commit), lanes
@@ -1273,6 +1308,22 @@ int launch_imap(const pncxk_args *a, const pncxk_imap *m, int gather) {
     hipStream_t st = (hipStream_t)a->stream;
     TransposeGeom g;
     const bool want = may_range<Op>::value && a->status != nullptr;
+    if constexpr (!Op::PRESERVE) {
+        constexpr int W = Op::SS > Op::DS ? Op::SS : Op::DS, E = 16 / W;    // elements per vector
+        const int ues = gather ? Op::SS : Op::DS, pes = gather ? Op::DS : Op::SS;
+        const int64_t uvb = (int64_t)E * ues, pvb = (int64_t)E * pes;         // vector bytes, user / packed side
+        const uint8_t *ubase = gather ? src : dst, *pbase = gather ? dst : src;
+        if (m->tmode == 1 && m->ndims == 1 && m->imap[0] == 1 && urun_enabled() && m->tlen % E == 0 &&
+            a->n % E == 0 && m->tn < (1LL << 32) && ((uintptr_t)ubase + (uintptr_t)m->tdisp0) % (uintptr_t)uvb == 0 &&
+            m->tstride % uvb == 0 && m->textent % uvb == 0 && (uintptr_t)pbase % (uintptr_t)pvb == 0) {
+            const int64_t nvec = a->n / E;
+            const unsigned grid = (unsigned)((nvec + 255) / 256 < MAX_BLOCKS ? (nvec + 255) / 256 : MAX_BLOCKS);
+            const Sink sk = sink_acquire(a->status, NC_ERANGE, st, grid, want);
+            if (gather) hipLaunchKernelGGL((k_urun<Op, true>), dim3(grid), dim3(256), 0, st, src, dst, nvec, *m, fill, sk);
+            else hipLaunchKernelGGL((k_urun<Op, false>), dim3(grid), dim3(256), 0, st, src, dst, nvec, *m, fill, sk);
+            return sink_finish(sk, st, grid, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
+        }
+    }
     // run-major: long-run tables in packed order, and uniform runs of 256..4096
     // elements in packed order (one wave per run instead of a division per
     // element; with 64-element runs the per-wave setup made it slower:

@@ -288,6 +288,11 @@ int xpose_merge() {     // read per launch: tests run both tilings in one proces
     return e == nullptr || atoi(e) != 0;
 }
 
+int urun_enabled() {     // read per launch: tests run both paths in one process
+    const char *e = getenv("PNCX_URUN");
+    return e == nullptr || atoi(e) != 0;
+}
+
 int fuse_lanes() {     // read per launch, so tests can run both shapes in one process
     const char *e = getenv("PNCX_FUSE_LANES");
     return (e != nullptr && atoi(e) == 1024) ? 1024 : 256;

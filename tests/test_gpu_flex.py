@@ -262,3 +262,20 @@ def test_flex_short_runs_many_steps(torch_cuda, xt, it):
     dt = run_case(torch_cuda, "dev", xt, it, disp.tolist(), blen.tolist(), int(disp[-1] + blen[-1] + 2), 12,
                   None, None, 31)
     assert dt.inq()["layout"] == 2
+
+
+@pytest.mark.parametrize("urun", ["1", "0"])
+@pytest.mark.parametrize("blen,gap", [(2, 2), (64, 16), (300, 4), (3, 1)])
+@pytest.mark.parametrize("xt,it", [(T.NC_DOUBLE, T.ITYPE_DOUBLE), (T.NC_FLOAT, T.ITYPE_DOUBLE),
+                                   (T.NC_SHORT, T.ITYPE_INT), (T.NC_INT, T.ITYPE_SHORT)])
+@pytest.mark.parametrize("where", ["host", "dev"])
+def test_flex_uniform_vector_runs(torch_cuda, where, xt, it, blen, gap, urun, monkeypatch):
+    """uniform runs whose lengths hold whole 16-byte vectors, 16-byte aligned,
+    over a contiguous count: one vector per lane (k_urun; PNCX_URUN=0 takes
+    k_imap / k_tmap_runs).  blen 3 does not divide into vectors and falls
+    back either way.  3 copies, NC_ERANGE from int -> NC_SHORT."""
+    monkeypatch.setenv("PNCX_URUN", urun)
+    nb = 4096 if blen <= 64 else 64
+    disp = (np.arange(nb) * (blen + gap)).tolist()
+    dt = run_case(torch_cuda, where, xt, it, disp, [blen] * nb, nb * (blen + gap), 3, None, None, 40 + blen)
+    assert dt.inq()["layout"] == 1
