@@ -5,6 +5,9 @@
 // bits as stored).  k_tile gives each 256-lane block one tile (a one-shot
 // grid; lanes loop only past 2^23 blocks) shaped by Shape<Op>: every global
 // load and store instruction of a wave covers one contiguous 1 KiB.
+// The range-tested and byte-source 2:1 widening ops run two tiles per block
+// (k_tile_u, Shape::TILE_U); the sign-bit byte classes convert a word at a
+// time (swar_conv).
 // The kernels are HBM-bound (no contraction: no MFMA).  LDS stages the
 // narrow side of 4:1 / 8:1 widening and of narrowing tiles (Shape below).
 //
