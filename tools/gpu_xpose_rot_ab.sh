@@ -1,6 +1,7 @@
 # A/B of the per-XCD start offset of the varm transpose (PNCX_XPOSE_ROT),
 # 2-D and 3-D shapes, both directions; the imap parity tests first.
 #   bash tools/gpu_xpose_rot_ab.sh <tag>
+# (PNCX_XPOSE_ROT existed only in the A/B build; the product has no rotation.)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/xrot_$1
