@@ -497,6 +497,7 @@ template <> struct VecT<16> { typedef uint32_t type __attribute__((ext_vector_ty
 template <> struct VecT<8> { typedef uint32_t type __attribute__((ext_vector_type(2))); };
 template <> struct VecT<4> { typedef uint32_t type; };
 template <> struct VecT<2> { typedef uint16_t type; };
+template <> struct VecT<1> { typedef uint8_t type; };
 
 template <int B, bool NT>
 __device__ __forceinline__ typename VecT<B>::type ldv(const uint8_t *p) {
@@ -955,17 +956,26 @@ __global__ __launch_bounds__(256) void k_urun(const uint8_t *src, uint8_t *dst, 
 }
 
 int urun_enabled();   // PNCX_URUN (default 1)
+int tmap_vec();       // PNCX_TMAP_VEC (default 1)
 
 // Derived buftype in packed order with long runs (tmode 3, or uniform runs
 // of 256..4096 elements, tmode 1): one wave per run
 // piece (pieces of at most PNCX_TMAP_PIECE elements, split at commit), lanes
 // along the piece -- both sides contiguous, no search.  c = copy, b = piece.
-template <class Op, bool GATHER>
+// VEC: a lane moves V = 16 / (wider element size) consecutive elements of
+// the piece with one 16-byte access on the wider side (runs start at any
+// element offset: unaligned vector accesses, legal on gfx950 global memory,
+// as ld_unaligned already relies on); the piece's last len % V elements go
+// one per lane.  PNCX_TMAP_VEC=0 moves one element per lane (A/B).
+template <class Op, bool GATHER, bool VEC = false>
 __global__ __launch_bounds__(256) void k_tmap_runs(const uint8_t *src, uint8_t *dst, int64_t n, pncxk_imap m,
                                                    typename Op::fill_t fill, Sink sk) {
     using SU = typename Op::SU;
     using DU = typename Op::DU;
     constexpr int UES = GATHER ? Op::SS : Op::DS;
+    constexpr int V = VEC && !Op::PRESERVE ? 16 / (Op::SS > Op::DS ? Op::SS : Op::DS) : 1;
+    using SV = typename VecT<V * Op::SS>::type;
+    using DV = typename VecT<V * Op::DS>::type;
     const int lane = threadIdx.x & 63;
     const int64_t total = n / m.tn * m.tnblk;            // pieces over all copies
     const int64_t nw = (int64_t)gridDim.x * 4;
@@ -977,7 +987,33 @@ __global__ __launch_bounds__(256) void k_tmap_runs(const uint8_t *src, uint8_t *
         const int64_t len = m.tmode == 1 ? m.tlen : m.tpre[b + 1] - p0;
         const int64_t ub = c * m.textent + (m.tmode == 1 ? m.tdisp0 + b * m.tstride : m.tdisp[b]);
         const int64_t kb = c * m.tn + p0;                   // packed element of the piece
-        for (int64_t e0 = lane; e0 < len; e0 += 64 * IMAP_U) {     // loads first (clamped), then stores
+        int64_t done = 0;
+        if constexpr (V > 1) {
+            const int64_t ng = len / V;                     // whole vectors of the piece
+            for (int64_t g0 = lane; g0 < ng; g0 += 64 * IMAP_U) {
+                SV sv[IMAP_U];
+#pragma unroll
+                for (int i = 0; i < IMAP_U; i++) {
+                    const int64_t e = (g0 + 64 * i < ng ? g0 + 64 * i : ng - 1) * V;
+                    sv[i] = ld_unaligned<SV>(GATHER ? src + ub + e * UES : src + (kb + e) * Op::SS);
+                }
+#pragma unroll
+                for (int i = 0; i < IMAP_U; i++) {
+                    const int64_t e = (g0 + 64 * i) * V;
+                    if (g0 + 64 * i < ng) {
+                        alignas(16) uint8_t sb[V * Op::SS];
+                        alignas(16) uint8_t db[V * Op::DS];
+                        __builtin_memcpy(sb, &sv[i], sizeof sb);
+                        conv_regs<Op, V>(sb, db, fill, bad);
+                        DV o;
+                        __builtin_memcpy(&o, db, sizeof o);
+                        st_unaligned<DV>(GATHER ? dst + (kb + e) * Op::DS : dst + ub + e * UES, o);
+                    }
+                }
+            }
+            done = ng * V;
+        }
+        for (int64_t e0 = done + lane; e0 < len; e0 += 64 * IMAP_U) {     // loads first (clamped), then stores
             SU sv[IMAP_U];
             DU old[IMAP_U];
 #pragma unroll
@@ -1335,8 +1371,14 @@ int launch_imap(const pncxk_args *a, const pncxk_imap *m, int gather) {
         const int64_t pieces = a->n / m->tn * m->tnblk;
         const unsigned grid = (unsigned)((pieces + 3) / 4 < MAX_BLOCKS ? (pieces + 3) / 4 : MAX_BLOCKS);
         const Sink sk = sink_acquire(a->status, NC_ERANGE, st, grid, want);
-        if (gather) hipLaunchKernelGGL((k_tmap_runs<Op, true>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, sk);
-        else hipLaunchKernelGGL((k_tmap_runs<Op, false>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, sk);
+        const bool vec = !Op::PRESERVE && tmap_vec();
+        if (gather) {
+            if (vec) hipLaunchKernelGGL((k_tmap_runs<Op, true, true>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, sk);
+            else hipLaunchKernelGGL((k_tmap_runs<Op, true>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, sk);
+        } else {
+            if (vec) hipLaunchKernelGGL((k_tmap_runs<Op, false, true>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, sk);
+            else hipLaunchKernelGGL((k_tmap_runs<Op, false>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, sk);
+        }
         return sink_finish(sk, st, grid, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
     }
     const int ues = gather ? Op::SS : Op::DS, pes = gather ? Op::DS : Op::SS;

@@ -293,6 +293,11 @@ int urun_enabled() {     // read per launch: tests run both paths in one process
     return e == nullptr || atoi(e) != 0;
 }
 
+int tmap_vec() {
+    const char *e = getenv("PNCX_TMAP_VEC");
+    return e == nullptr || atoi(e) != 0;
+}
+
 int fuse_lanes() {     // read per launch, so tests can run both shapes in one process
     const char *e = getenv("PNCX_FUSE_LANES");
     return (e != nullptr && atoi(e) == 1024) ? 1024 : 256;
