@@ -955,6 +955,36 @@ __global__ __launch_bounds__(256) void k_urun(const uint8_t *src, uint8_t *dst, 
     publish(sk, sk.status, bad);
 }
 
+// varm whose fastest dimension is contiguous in the user buffer (imap 1,
+// e.g. a padded array's interior) and holds whole vectors (count % V == 0,
+// V = 16 / wider element size): a lane moves V elements of one row with one
+// imap decode and one (possibly unaligned) 16-byte access on the wider side;
+// k_imap decodes and moves one element per lane.  PNCX_IMAP_ROWS=0 (A/B).
+template <class Op, bool GATHER, typename IDX>
+__global__ __launch_bounds__(256) void k_imap_rows(const uint8_t *src, uint8_t *dst, int64_t nvec, pncxk_imap m,
+                                                   typename Op::fill_t fill, Sink sk) {
+    constexpr int SS = Op::SS, DS = Op::DS, W = SS > DS ? SS : DS, V = 16 / W;
+    constexpr int UES = GATHER ? SS : DS;
+    using SV = typename VecT<V * SS>::type;
+    using DV = typename VecT<V * DS>::type;
+    bool bad = false;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t v = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 256 + threadIdx.x; v < nvec; v += stride) {
+        const int64_t k = v * V;
+        const int64_t ub = imap_offset<IDX>((IDX)k, m) * UES;
+        const SV x = ld_unaligned<SV>(GATHER ? src + ub : src + k * SS);
+        alignas(16) uint8_t sb[V * SS];
+        alignas(16) uint8_t db[V * DS];
+        __builtin_memcpy(sb, &x, sizeof sb);
+        conv_regs<Op, V>(sb, db, fill, bad);
+        DV o;
+        __builtin_memcpy(&o, db, sizeof o);
+        st_unaligned<DV>(GATHER ? dst + k * DS : dst + ub, o);
+    }
+    publish(sk, sk.status, bad);
+}
+
+int imap_rows();      // PNCX_IMAP_ROWS (default 1)
 int urun_enabled();   // PNCX_URUN (default 1)
 int tmap_vec();       // PNCX_TMAP_VEC (default 1)
 
@@ -1399,8 +1429,25 @@ int launch_imap(const pncxk_args *a, const pncxk_imap *m, int gather) {
         }
         return sink_finish(sk, st, grid, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
     }
-    const int grid = launch_grid(a->n, 4);
     const bool small = a->n < (1LL << 32) && m->max_count < (1LL << 32);
+    if constexpr (!Op::PRESERVE) {
+        constexpr int V = 16 / (Op::SS > Op::DS ? Op::SS : Op::DS);
+        if (V > 1 && m->tmode == 0 && m->ndims > 1 && m->imap[m->ndims - 1] == 1 && m->count[m->ndims - 1] % V == 0 &&
+            imap_rows()) {
+            const int64_t nvec = a->n / V;
+            const unsigned grid = (unsigned)((nvec + 255) / 256 < MAX_BLOCKS ? (nvec + 255) / 256 : MAX_BLOCKS);
+            const Sink sk = sink_acquire(a->status, NC_ERANGE, st, grid, want);
+            if (gather) {
+                if (small) hipLaunchKernelGGL((k_imap_rows<Op, true, uint32_t>), dim3(grid), dim3(256), 0, st, src, dst, nvec, *m, fill, sk);
+                else hipLaunchKernelGGL((k_imap_rows<Op, true, uint64_t>), dim3(grid), dim3(256), 0, st, src, dst, nvec, *m, fill, sk);
+            } else {
+                if (small) hipLaunchKernelGGL((k_imap_rows<Op, false, uint32_t>), dim3(grid), dim3(256), 0, st, src, dst, nvec, *m, fill, sk);
+                else hipLaunchKernelGGL((k_imap_rows<Op, false, uint64_t>), dim3(grid), dim3(256), 0, st, src, dst, nvec, *m, fill, sk);
+            }
+            return sink_finish(sk, st, grid, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
+        }
+    }
+    const int grid = launch_grid(a->n, 4);
     const Sink sk = sink_acquire(a->status, NC_ERANGE, st, grid, want);
     if (gather) {
         if (small) hipLaunchKernelGGL((k_imap<Op, true, uint32_t>), dim3(grid), dim3(256), 0, st, src, dst, a->n, *m, fill, sk);

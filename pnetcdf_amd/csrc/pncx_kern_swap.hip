@@ -298,6 +298,11 @@ int tmap_vec() {
     return e == nullptr || atoi(e) != 0;
 }
 
+int imap_rows() {
+    const char *e = getenv("PNCX_IMAP_ROWS");
+    return e == nullptr || atoi(e) != 0;
+}
+
 int fuse_lanes() {     // read per launch, so tests can run both shapes in one process
     const char *e = getenv("PNCX_FUSE_LANES");
     return (e != nullptr && atoi(e) == 1024) ? 1024 : 256;

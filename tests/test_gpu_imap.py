@@ -170,3 +170,27 @@ def test_imap_tile_merged_dims(torch_cuda, count, imap, xt, it, merge, monkeypat
     numpy gather/scatter + the oracle, on device buffers."""
     monkeypatch.setenv("PNCX_XPOSE_MERGE", merge)
     test_imap_put_get(torch_cuda, count, imap, xt, it, "dev")
+
+
+# varm with a contiguous fastest dimension holding whole 16-byte vectors
+# (k_imap_rows): padded rows of a 3-D interior, a 2-D row gather, and a
+# count that is not a multiple of the vector (falls back to k_imap)
+ROW_CASES = [
+    ([6, 5, 34], [1000, 40, 1]),
+    ([9, 18], [20, 1]),
+    ([7, 13], [16, 1]),
+    ([3, 4, 64], [4096, 70, 1]),
+]
+
+
+@pytest.mark.parametrize("count,imap", ROW_CASES)
+@pytest.mark.parametrize("xt,it", [(T.NC_DOUBLE, T.ITYPE_DOUBLE), (T.NC_INT, T.ITYPE_DOUBLE), (T.NC_SHORT, T.ITYPE_INT),
+                                   (T.NC_BYTE, T.ITYPE_UCHAR), (T.NC_FLOAT, T.ITYPE_FLOAT)])
+@pytest.mark.parametrize("rows", ["1", "0"])
+def test_imap_contiguous_rows(torch_cuda, count, imap, xt, it, rows, monkeypatch):
+    """varm rows contiguous in the user buffer, a vector per lane
+    (PNCX_IMAP_ROWS=1, default) or an element per lane (0): put and get
+    against a numpy gather/scatter + the oracle, host and device buffers"""
+    monkeypatch.setenv("PNCX_IMAP_ROWS", rows)
+    for where in ("host", "dev"):
+        test_imap_put_get(torch_cuda, count, imap, xt, it, where)

@@ -6,6 +6,7 @@ runs are not counted).
 Workloads (NC_DOUBLE external <- double user buffer, put direction):
   halo3d    interior 254^3 of a 256^3 local array (ghost cells dropped): a 3-D
             subarray buftype, 64516 runs of 254 elements -> general table
+  halo3d_varm  the same interior as a varm request (imap {L*L, L, 1})
   vector2   every other element (MPI_Type_vector(n, 1, 2)) -> uniform runs
   vector64  runs of 64 every 80 -> uniform runs
   vector256 runs of 256 every 272 -> uniform runs, one wave per run
@@ -75,6 +76,14 @@ def main():
     res.append(("halo3d", dt.inq()["layout"], n) + timeit(
         lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(xb.data_ptr()), ctypes.c_void_p(ub.data_ptr()),
                                        1, cp, None, 1, dt.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n))
+    # the same interior through varm (imap {L*L, L, 1} from the first interior element)
+    cv, cvp = offs([I, I, I])
+    iv, ivp = offs([L * L, L, 1])
+    first = ((L * L + L + 1) * 8)
+    res.append(("halo3d_varm", -1, n) + timeit(
+        lambda: lib.pncx_dev_putn_imap(5, T.NC_DOUBLE, ctypes.c_void_p(xb.data_ptr()),
+                                       ctypes.c_void_p(ub.data_ptr() + first), 3, cvp, ivp, T.ITYPE_DOUBLE, fp,
+                                       ctypes.c_void_p(st.data_ptr()), sp), n))
     res.append(("contig", -1, n) + timeit(
         lambda: lib.pncx_dev_putn(5, T.NC_DOUBLE, ctypes.c_void_p(xb.data_ptr()), ctypes.c_void_p(ub.data_ptr()), n,
                                   T.ITYPE_DOUBLE, fp, ctypes.c_void_p(st.data_ptr()), sp), n))
