@@ -803,6 +803,9 @@ struct pncx_dtype {
                                        * (off16) one base per 64-element chunk
                                        * followed by 16-bit offsets from it (tmode 5) */
     int        off16;
+    long long  rn1, rn2, rs1, rs2;    /* table runs on a 2-level lattice: run i at
+                                       * disp0 + (i % rn1)*rs1 + (i / rn1)*rs2 bytes
+                                       * (rn1 = 0: not one) */
 };
 
 /* Largest typemap (elements per copy) that gets a per-element offset map:
@@ -869,6 +872,29 @@ int pncx_type_commit(int itype, pncx_offset nblocks, const pncx_offset *disp,
         t->disp0 = t->disp[0];
         t->stride = k > 1 ? t->disp[1] - t->disp[0] : 0;
         t->layout = uniform ? 1 : 2;
+    }
+    /* a table whose equal-length runs sit on a 2-level lattice (a 3-D
+     * subarray: rows, then planes) is also an imap; flex_layout can then take
+     * the varm kernels (k_imap_rows) instead of the run-piece kernel */
+    if (t->layout == 2 && k > 2) {
+        long long n1 = 1, i2;
+        int ok = 1;
+        const long long s1 = t->disp[1] - t->disp[0];
+        for (i = 1; i < k && ok; i++) ok = len[i] == len[0];
+        while (n1 < k && t->disp[n1] - t->disp[n1 - 1] == s1) n1++;
+        ok = ok && n1 > 1 && n1 < k && k % n1 == 0 && s1 > 0;
+        if (ok) {
+            const long long s2 = t->disp[n1] - t->disp[0];
+            for (i2 = 0; i2 < k && ok; i2++)
+                ok = t->disp[i2] == t->disp[0] + (i2 % n1) * s1 + (i2 / n1) * s2;
+            ok = ok && s2 > 0 && s1 % isz == 0 && s2 % isz == 0 && t->disp[0] % isz == 0 && extent % isz == 0;
+            if (ok) {
+                t->rn1 = n1;
+                t->rn2 = k / n1;
+                t->rs1 = s1;
+                t->rs2 = s2;
+            }
+        }
     }
     free(len);
     if (t->layout == 2 && have_device()) {
@@ -1013,10 +1039,28 @@ int pncx_type_inq(const pncx_dtype *t, int *itype, pncx_offset *nelems, pncx_off
  * apply), 1 when the fused typemap kernel is needed (m filled, user bytes in
  * [*lo, *hi) relative to buf), -1 with *err set on a bad argument.
  */
+/* elements of one 16-byte vector of the conversion (0: the NULL-fill
+ * codecs, which k_imap_rows does not take) */
+static int flex_vec(const op_t *op)
+{
+    const int w = op->ss > op->ds ? op->ss : op->ds;
+    return op->c || w <= 0 ? 0 : 16 / w;
+}
+
+/* PNCX_TMAP_IMAP=0 keeps lattice tables on the run-piece kernel (A/B) */
+static int tmap_imap_enabled(void)
+{
+    const char *e = getenv("PNCX_TMAP_IMAP");
+    return e == NULL || atoi(e) != 0;
+}
+
+/* vec: elements per 16-byte vector of the call's conversion (0: none);
+ * *koff: bytes to add to the user pointer handed to the kernel */
 static int flex_layout(int ndims, const pncx_offset *count, const pncx_offset *imap, long long bufcount,
                        const pncx_dtype *t, pncxk_imap *m, long long *n, long long *lo, long long *hi,
-                       int *err)
+                       int *err, int vec, long long *koff)
 {
+    *koff = 0;
     long long span;
     *lo = *hi = 0;
     if (t == NULL || bufcount < 0) { *err = NC_EINVAL; return -1; }
@@ -1033,6 +1077,25 @@ static int flex_layout(int ndims, const pncx_offset *count, const pncx_offset *i
     if (t->layout == 0 || (t->nblk == 1 && bufcount == 1)) {
         *lo = t->nblk ? t->disp0 : 0;
         return 0;
+    }
+    if (packed_order && t->layout == 2 && t->rn1 > 0 && vec > 1 && t->len % vec == 0 && tmap_imap_enabled()) {
+        /* lattice table over a contiguous count: copies x planes x rows x
+         * run, as an imap from the first run (k_imap_rows) */
+        const long long isz = t->isz;
+        m->ndims = 4;
+        m->count[0] = bufcount; m->count[1] = t->rn2; m->count[2] = t->rn1; m->count[3] = t->len;
+        m->imap[0] = t->extent / isz; m->imap[1] = t->rs2 / isz; m->imap[2] = t->rs1 / isz; m->imap[3] = 1;
+        m->max_count = bufcount > t->rn2 ? bufcount : t->rn2;
+        if (t->rn1 > m->max_count) m->max_count = t->rn1;
+        if (t->len > m->max_count) m->max_count = t->len;
+        m->tmode = 0;
+        *koff = t->disp0;
+        {
+            const long long last = (bufcount - 1) * t->extent;
+            *lo = t->lo < last + t->lo ? t->lo : last + t->lo;
+            *hi = t->hi > last + t->hi ? t->hi : last + t->hi;
+        }
+        return 1;
     }
     m->tmode = t->layout == 2 && t->runmajor && packed_order ? 3
              : t->layout == 2 && t->doff ? (t->off16 ? 5 : 4) : t->layout;
@@ -1062,17 +1125,18 @@ int pncx_dev_putn_flex(int cdf_ver, int xtype, void *dxbuf, const void *dbuf, in
 {
     op_t op;
     pncxk_imap m;
-    long long n, lo, hi;
+    long long n, lo, hi, koff;
     int err, r;
     if (bt == NULL) return NC_EINVAL;
     if ((err = classify(PNCX_PUT, cdf_ver, xtype, bt->itype, fillp, &op)) != NC_NOERR) return err;
-    if ((r = flex_layout(ndims, count, imap, bufcount, bt, &m, &n, &lo, &hi, &err)) < 0) return err;
+    if ((r = flex_layout(ndims, count, imap, bufcount, bt, &m, &n, &lo, &hi, &err, flex_vec(&op), &koff)) < 0)
+        return err;
     if (r == 0)
         return pncx_dev_putn_imap(cdf_ver, xtype, dxbuf, (const char *)dbuf + lo, ndims, count, imap,
                                   bt->itype, fillp, dstatus, stream);
     if (n <= 0) return NC_NOERR;
     if (!have_device() || (m.tmode >= 2 && m.tpre == NULL)) return PNCX_EDEVICE;
-    return launch_imap_op(&op, dbuf, dxbuf, n, &m, 1, dstatus, stream);
+    return launch_imap_op(&op, (const char *)dbuf + koff, dxbuf, n, &m, 1, dstatus, stream);
 }
 
 int pncx_dev_getn_flex(int cdf_ver, int xtype, const void *dxbuf, void *dbuf, int ndims,
@@ -1081,17 +1145,18 @@ int pncx_dev_getn_flex(int cdf_ver, int xtype, const void *dxbuf, void *dbuf, in
 {
     op_t op;
     pncxk_imap m;
-    long long n, lo, hi;
+    long long n, lo, hi, koff;
     int err, r;
     if (bt == NULL) return NC_EINVAL;
     if ((err = classify(PNCX_GET, cdf_ver, xtype, bt->itype, NULL, &op)) != NC_NOERR) return err;
-    if ((r = flex_layout(ndims, count, imap, bufcount, bt, &m, &n, &lo, &hi, &err)) < 0) return err;
+    if ((r = flex_layout(ndims, count, imap, bufcount, bt, &m, &n, &lo, &hi, &err, flex_vec(&op), &koff)) < 0)
+        return err;
     if (r == 0)
         return pncx_dev_getn_imap(cdf_ver, xtype, dxbuf, (char *)dbuf + lo, ndims, count, imap,
                                   bt->itype, dstatus, stream);
     if (n <= 0) return NC_NOERR;
     if (!have_device() || (m.tmode >= 2 && m.tpre == NULL)) return PNCX_EDEVICE;
-    return launch_imap_op(&op, dxbuf, dbuf, n, &m, 0, dstatus, stream);
+    return launch_imap_op(&op, dxbuf, (char *)dbuf + koff, n, &m, 0, dstatus, stream);
 }
 
 /* host buffers: stage the user byte span [lo, hi) and the packed buffer */
@@ -1101,7 +1166,7 @@ static int host_flex(int dir, int cdf_ver, int xtype, void *xbuf, void *buf, int
 {
     op_t op;
     pncxk_imap m;
-    long long n, lo, hi;
+    long long n, lo, hi, koff;
     ctx_t *c;
     int err, r, st = 0;
     pinned_t pn = {{NULL, NULL}, 0};
@@ -1110,7 +1175,8 @@ static int host_flex(int dir, int cdf_ver, int xtype, void *xbuf, void *buf, int
     void *s;
     if (bt == NULL) return NC_EINVAL;
     if ((err = classify(dir, cdf_ver, xtype, bt->itype, fillp, &op)) != NC_NOERR) return err;
-    if ((r = flex_layout(ndims, count, imap, bufcount, bt, &m, &n, &lo, &hi, &err)) < 0) return err;
+    if ((r = flex_layout(ndims, count, imap, bufcount, bt, &m, &n, &lo, &hi, &err, flex_vec(&op), &koff)) < 0)
+        return err;
     if (r == 0)
         return dir == PNCX_PUT
                    ? pncx_putn_imap(cdf_ver, xtype, xbuf, (const char *)buf + lo, ndims, count, imap, bt->itype, fillp)
@@ -1134,11 +1200,11 @@ static int host_flex(int dir, int cdf_ver, int xtype, void *xbuf, void *buf, int
     if (!err) err = pncxrt_memcpy_h2d(du, ubase, ub, s);       /* user span (get: keeps the holes) */
     if (dir == PNCX_PUT) {
         if (!err && op.c) err = pncxrt_memcpy_h2d(dx, xbuf, (size_t)n * xs, s);
-        if (!err) err = launch_imap_op(&op, du - lo, dx, n, &m, 1, c->dstatus, s);
+        if (!err) err = launch_imap_op(&op, du - lo + koff, dx, n, &m, 1, c->dstatus, s);
         if (!err) err = pncxrt_memcpy_d2h(xbuf, dx, (size_t)n * xs, s);
     } else {
         if (!err) err = pncxrt_memcpy_h2d(dx, xbuf, (size_t)n * xs, s);
-        if (!err) err = launch_imap_op(&op, dx, du - lo, n, &m, 0, c->dstatus, s);
+        if (!err) err = launch_imap_op(&op, dx, du - lo + koff, n, &m, 0, c->dstatus, s);
         if (!err) err = pncxrt_memcpy_d2h(ubase, du, ub, s);
     }
     if (!err) err = pncxrt_memcpy_d2h(&st, c->dstatus, sizeof(int), s);

@@ -279,3 +279,22 @@ def test_flex_uniform_vector_runs(torch_cuda, where, xt, it, blen, gap, urun, mo
     disp = (np.arange(nb) * (blen + gap)).tolist()
     dt = run_case(torch_cuda, where, xt, it, disp, [blen] * nb, nb * (blen + gap), 3, None, None, 40 + blen)
     assert dt.inq()["layout"] == 1
+
+
+@pytest.mark.parametrize("tmap_imap", ["1", "0"])
+@pytest.mark.parametrize("xt,it", [(T.NC_DOUBLE, T.ITYPE_DOUBLE), (T.NC_INT, T.ITYPE_DOUBLE), (T.NC_SHORT, T.ITYPE_INT),
+                                   (T.NC_FLOAT, T.ITYPE_FLOAT), (T.NC_BYTE, T.ITYPE_UCHAR)])
+@pytest.mark.parametrize("where", ["host", "dev"])
+@pytest.mark.parametrize("ghost", [1, 2])
+def test_flex_lattice_subarray(torch_cuda, where, xt, it, tmap_imap, ghost, monkeypatch):
+    """a 3-D subarray buftype (interior of a ghosted block: equal runs on a
+    2-level lattice) x 2 copies: with PNCX_TMAP_IMAP=1 (default) it runs as a
+    4-D varm over the first run (k_imap_rows) when its rows hold whole
+    vectors, else through the run-piece kernel; both against numpy + oracle"""
+    monkeypatch.setenv("PNCX_TMAP_IMAP", tmap_imap)
+    L = (9, 10, 12)
+    z, y = np.meshgrid(np.arange(L[0] - 2 * ghost), np.arange(L[1] - 2 * ghost), indexing="ij")
+    disp = (((z + ghost) * L[1] * L[2] + (y + ghost) * L[2] + ghost)).reshape(-1).tolist()
+    blen = [L[2] - 2 * ghost] * len(disp)
+    dt = run_case(torch_cuda, where, xt, it, disp, blen, L[0] * L[1] * L[2], 2, None, None, 60 + ghost)
+    assert dt.inq()["layout"] == 2
