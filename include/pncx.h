@@ -331,6 +331,25 @@ int pncx_dev_batch_async(const pncx_seg *segs, int nseg, int *dstatus,
 int pncx_dev_batch_timing(int enable);
 int pncx_dev_batch_kernel_ms(double *total_ms, long long *calls);
 
+/* Measurement aid (no reference counterpart): per-phase time of the
+ * host-buffer paths (pncx_putn/getn/in_swapn and the file layer's blocking
+ * put/get from host buffers).  Off by default, or on from the start with
+ * PNCX_PHASES=1 in the environment.  pncx_phases(1) clears the sums and
+ * turns recording on, pncx_phases(0) turns it off.  Phase ids run from 0
+ * while pncx_phase_name(id) is not NULL; a phase's host time is summed in
+ * microseconds with the number of times it ran.  Phases named "gpu.*" are
+ * HIP-event intervals on the device (H2D, kernel, D2H), the others host
+ * clock intervals. */
+int pncx_phases(int enable);
+/* A/B switches of the kernel and staging choices (DESIGN.md names each):
+ * PNCX_<name> in the environment is read once when the library loads; this
+ * changes one for the calls that follow (value -1 restores the default).
+ * NC_EINVAL for an unknown name. */
+int pncx_knob_set(const char *name, long long value);
+int pncx_knob_get(const char *name, long long *value);
+const char *pncx_phase_name(int id);
+int pncx_phase_read(int id, double *us, long long *count);
+
 /* Host buffers (staged through HBM). */
 int pncx_batch(const pncx_seg *segs, int nseg, int *status_out);
 

@@ -10,12 +10,15 @@
  */
 #include <pthread.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
 
 #include "../../include/pncx.h"
 #include "pncx_shim.h"
+#include "pncx_phase.h"
+#include "pncx_stage.h"
 
 /* ------------------------------------------------------------------------ */
 /* type metadata                                                             */
@@ -85,6 +88,110 @@ const char *pncx_strerror(int err)
 }
 
 const char *pncx_version(void) { return "pncx 0.1 gfx950 (swap 2/4/8/n, 10x11 get/put, batch)"; }
+
+/* ------------------------------------------------------------------------ */
+/* per-phase timing (pncx_phase.h; pncx_phases in include/pncx.h)            */
+/* ------------------------------------------------------------------------ */
+int pncx_ph_on;
+static double g_ph_us[PH_N];
+static long long g_ph_n[PH_N];
+static pthread_mutex_t g_ph_lock = PTHREAD_MUTEX_INITIALIZER;
+static const char *const g_ph_names[PH_N] = {
+    "put.plan", "put.register", "put.convert", "put.write", "put.wait", "put.unregister", "put.total",
+    "get.plan", "get.register", "get.read", "get.convert", "get.unregister", "get.total",
+    "conv.lock_pin", "conv.enqueue", "conv.sync", "conv.status", "conv.unpin",
+    "gpu.h2d", "gpu.kernel", "gpu.d2h"};
+
+/* A/B knobs (pncx_shim.h): the environment once at load, then pncx_knob_set */
+static const char *const g_knob_names[PNCXK_NKNOB] = {
+    "TILE_U", "XPOSE_MERGE", "URUN", "TMAP_VEC", "IMAP_ROWS", "FUSE_LANES", "BATCH_FUSE", "TMAP_IMAP",
+    "TOFF16", "TOFF_MAX_ELEMS", "XPOSE_ORDER", "TOFF_RUNS", "HOST_ZC"};
+static long long g_knob[PNCXK_NKNOB];
+
+long long pncx_knob(int id)
+{
+    return id >= 0 && id < PNCXK_NKNOB ? __atomic_load_n(&g_knob[id], __ATOMIC_RELAXED) : -1;
+}
+
+static int knob_id(const char *name)
+{
+    int i;
+    if (name == NULL) return -1;
+    if (strncmp(name, "PNCX_", 5) == 0) name += 5;
+    for (i = 0; i < PNCXK_NKNOB; i++)
+        if (strcmp(name, g_knob_names[i]) == 0) return i;
+    return -1;
+}
+
+int pncx_knob_set(const char *name, long long value)
+{
+    const int id = knob_id(name);
+    if (id < 0) return NC_EINVAL;
+    __atomic_store_n(&g_knob[id], value < 0 ? -1 : value, __ATOMIC_RELAXED);
+    return NC_NOERR;
+}
+
+int pncx_knob_get(const char *name, long long *value)
+{
+    const int id = knob_id(name);
+    if (id < 0) return NC_EINVAL;
+    if (value) *value = pncx_knob(id);
+    return NC_NOERR;
+}
+
+__attribute__((constructor)) static void ph_init(void)
+{
+    const char *e = getenv("PNCX_PHASES");
+    char nm[64];
+    int i;
+    pncx_ph_on = e != NULL && atoi(e) != 0;
+    for (i = 0; i < PNCXK_NKNOB; i++) {
+        snprintf(nm, sizeof nm, "PNCX_%s", g_knob_names[i]);
+        e = getenv(nm);
+        g_knob[i] = (e != NULL && e[0] != '\0') ? atoll(e) : -1;
+        if (g_knob[i] < -1) g_knob[i] = -1;
+    }
+}
+
+double pncx_ph_now(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec * 1e6 + (double)t.tv_nsec * 1e-3;
+}
+
+void pncx_ph_add_us(int id, double us)
+{
+    if (id < 0 || id >= PH_N) return;
+    pthread_mutex_lock(&g_ph_lock);
+    g_ph_us[id] += us;
+    g_ph_n[id]++;
+    pthread_mutex_unlock(&g_ph_lock);
+}
+
+int pncx_phases(int enable)
+{
+    pthread_mutex_lock(&g_ph_lock);
+    if (enable) {
+        memset(g_ph_us, 0, sizeof g_ph_us);
+        memset(g_ph_n, 0, sizeof g_ph_n);
+    }
+    pncx_ph_on = enable != 0;
+    pthread_mutex_unlock(&g_ph_lock);
+    return NC_NOERR;
+}
+
+const char *pncx_phase_name(int id) { return id >= 0 && id < PH_N ? g_ph_names[id] : NULL; }
+
+int pncx_phase_read(int id, double *us, long long *count)
+{
+    if (id < 0 || id >= PH_N) return NC_EINVAL;
+    pthread_mutex_lock(&g_ph_lock);
+    if (us) *us = g_ph_us[id];
+    if (count) *count = g_ph_n[id];
+    pthread_mutex_unlock(&g_ph_lock);
+    return NC_NOERR;
+}
 
 int pncx_device_count(void) { return pncxrt_device_count(); }
 int pncx_set_device(int dev) { return pncxrt_set_device(dev); }
@@ -273,6 +380,7 @@ int pncx_dev_status_read(const int *dstatus, pncx_stream_t stream)
 #define MAX_DEV 64
 
 #define NTEV 256              /* event pairs of pncx_dev_batch_timing read in one go */
+#define PH_EVCH 8             /* chunks per call given phase events */
 typedef struct ctx_t {
     int    init;
     void  *stream[NSLOT];
@@ -315,6 +423,13 @@ typedef struct ctx_t {
     double tms;               /* summed kernel time of the timed batch calls */
     long long tcalls;         /* ... and their number                         */
     unsigned long long *dfirst;   /* pncx_dev_first_diff result word */
+    void  *pev[4 * PH_EVCH];  /* pncx_phases: H2D / kernel / D2H events of the first chunks */
+    /* staged host-buffer calls (pncx_stage_*): a ring of device slots, an
+     * event per chunk after its kernel and after its D2H, a pinned status word */
+    void  *sdbuf[4];
+    size_t sdbuf_size;
+    void  *sev_conv[32], *sev_out[32];
+    int   *hstat;
 } ctx_t;
 
 static ctx_t g_ctx[MAX_DEV];
@@ -431,63 +546,240 @@ static void unpin_all(pinned_t *pn)
 }
 
 /*
- * Stage src (n elements of op->ss bytes, host) -> kernel -> dst (host).
- * Chunks alternate between two streams/slots: while chunk k's kernel runs,
- * chunk k-1's result streams back and chunk k+1's input streams in.
+ * Staged conversion of host buffers through HBM (pncx_stage.h).
+ *
+ * A call is cut into chunks.  Each chunk's input is copied to a device slot
+ * and converted on the "in" stream; its result is copied back on the "out"
+ * stream once the kernel's event has fired.  With the two copy directions
+ * on different streams, chunk k+1's H2D overlaps chunk k's D2H (PCIe is
+ * full duplex): a 4 MiB swap moves in ~1.3x one direction's copy time
+ * instead of 2x (tools/c1_probe.hip, profiles/r04a_c1_probe_4m.txt).  The
+ * caller can wait for chunk k alone (pncx_stage_wait) and hand it to file
+ * I/O while later chunks are still converting -- the file layer's put/get
+ * pipelines (pncx_nc.c).  The ring of NDBUF device slots is reused in
+ * order: chunk k's H2D waits for chunk k-NDBUF's D2H on the device.
+ *
  * preserve: the destination's current content is needed (NULL-fill codecs).
  */
+#define NDBUF 4
+#define NSEV 32                     /* chunks in flight (event ring)       */
+struct pncx_stage {
+    ctx_t *c;
+    op_t op;
+    int preserve, want_status;
+    long long chunk;                /* elements per device slot            */
+    size_t din_bytes;               /* input part of a slot                */
+    int pushed, waited;             /* chunks enqueued / known complete    */
+    int err;
+    pinned_t pn;
+    int ph_ev;
+};
+
+static int stage_slots(ctx_t *c, size_t slot_bytes)
+{
+    int i;
+    if (c->sev_out[NSEV - 1] == NULL)
+        for (i = 0; i < NSEV; i++)
+            if (pncxrt_event_create_fast(&c->sev_conv[i]) || pncxrt_event_create_fast(&c->sev_out[i]))
+                return PNCX_EDEVICE;
+    if (c->hstat == NULL && pncxrt_host_alloc((void **)&c->hstat, 64) != 0) return PNCX_EDEVICE;
+    if (c->sdbuf_size >= slot_bytes) return 0;
+    for (i = 0; i < NSLOT; i++) pncxrt_stream_sync(c->stream[i]);
+    for (i = 0; i < NDBUF; i++) {
+        pncxrt_free(c->sdbuf[i]);
+        c->sdbuf[i] = NULL;
+    }
+    c->sdbuf_size = 0;
+    for (i = 0; i < NDBUF; i++)
+        if (pncxrt_malloc(&c->sdbuf[i], slot_bytes) != 0) return PNCX_EDEVICE;
+    c->sdbuf_size = slot_bytes;
+    return 0;
+}
+
+/* elements per chunk for a call of n elements: about 4 chunks, each of
+ * 1 MiB of input + output at least, chunk_bytes() at most */
+static long long stage_chunk_elems(const op_t *op, long long n)
+{
+    const long long per = op->ss + op->ds;
+    long long lo = (1LL << 20) / per, hi = (long long)chunk_bytes() / per, c = (n + 3) / 4;
+    if (lo < 1) lo = 1;
+    if (hi < lo) hi = lo;
+    if (c < lo) c = lo;
+    if (c > hi) c = hi;
+    return c < n ? c : (n > 0 ? n : 1);
+}
+
+static int stage_open(pncx_stage **hp, const op_t *op, int preserve, long long max_chunk)
+{
+    pncx_stage *h;
+    ctx_t *c = get_ctx();
+    int err;
+    double t0 = PH_T0();
+    *hp = NULL;
+    if (c == NULL) return PNCX_EDEVICE;
+    if ((h = (pncx_stage *)calloc(1, sizeof *h)) == NULL) return NC_ENOMEM;
+    h->c = c;
+    h->op = *op;
+    h->preserve = preserve;
+    /* a same-type swap cannot report NC_ERANGE: no status word to zero or read */
+    h->want_status = op->kind != PNCXK_SWAP;
+    h->chunk = max_chunk > 0 ? max_chunk : 1;
+    h->din_bytes = ALIGN16((size_t)h->chunk * (size_t)op->ss);
+    pthread_mutex_lock(&c->lock);
+    err = stage_slots(c, h->din_bytes + ALIGN16((size_t)h->chunk * (size_t)op->ds));
+    if (!err && h->want_status) err = pncxrt_memset(c->dstatus, 0, sizeof(int), c->stream[0]);
+    if (!err && pncx_ph_on && c->pev[0] == NULL) {
+        int i;
+        for (i = 0; i < 4 * PH_EVCH; i++)
+            if (pncxrt_event_create(&c->pev[i]) != 0) { c->pev[i] = NULL; break; }
+    }
+    PH_ADD(PH_CONV_LOCK, t0);
+    if (err) {
+        pthread_mutex_unlock(&c->lock);
+        free(h);
+        return err;
+    }
+    *hp = h;
+    return NC_NOERR;
+}
+
+int pncx_stage_begin(pncx_stage **hp, int dir, int cdf_ver, int xtype, int itype, const void *fillp,
+                     long long max_chunk)
+{
+    op_t op;
+    int err;
+    if (hp) *hp = NULL;
+    if (hp == NULL) return NC_EINVAL;
+    if (dir == PNCX_SWAP_DIR) {
+        memset(&op, 0, sizeof op);
+        op.kind = PNCXK_SWAP;
+        op.a = op.ss = op.ds = xtype;           /* xtype carries the element size */
+        if (xtype < 1) return NC_EINVAL;
+    } else if ((err = classify(dir, cdf_ver, xtype, itype, fillp, &op)) != NC_NOERR) {
+        return err;
+    }
+    if (!have_device()) return PNCX_EDEVICE;
+    return stage_open(hp, &op, dir == PNCX_PUT ? op.c : 0, max_chunk);
+}
+
+/* enqueue n (<= the handle's chunk) elements src -> dst; returns the chunk
+ * index (>= 0) or an error (< 0) */
+int pncx_stage_push(pncx_stage *h, const void *src, void *dst, long long n)
+{
+    ctx_t *c = h->c;
+    const op_t *op = &h->op;
+    const int k = h->pushed, slot = k % NDBUF, e = k % NSEV;
+    uint8_t *din = (uint8_t *)c->sdbuf[slot], *dout = din + h->din_bytes;
+    void *si = c->stream[0], *so = c->stream[1];
+    void **ev = NULL;
+    int err = h->err;
+    double t0 = PH_T0();
+    if (err) return err;
+    if (n <= 0 || n > h->chunk) return NC_EINVAL;
+    if (k - h->waited >= NSEV) {                   /* the event ring is full: wait the oldest */
+        if ((err = pncx_stage_wait(h, k - NSEV)) != NC_NOERR) return err;
+    }
+    if (pncx_ph_on && c->pev[4 * PH_EVCH - 1] && h->ph_ev < PH_EVCH) ev = &c->pev[4 * h->ph_ev++];
+    if (op->ss == op->ds && src == dst) dout = din;            /* in-place swap */
+    /* the slot's previous chunk must be back on the host */
+    if (k >= NDBUF) err = pncxrt_stream_wait_event(si, c->sev_out[(k - NDBUF) % NSEV]);
+    if (!err && ev) err = pncxrt_event_record(ev[0], si);
+    if (!err) err = pncxrt_memcpy_h2d(din, src, (size_t)n * op->ss, si);
+    if (!err && h->preserve && dout != din) err = pncxrt_memcpy_h2d(dout, dst, (size_t)n * op->ds, si);
+    if (!err && ev) err = pncxrt_event_record(ev[1], si);
+    if (!err && !(op->kind == PNCXK_SWAP && op->a == 1 && dout == din))
+        err = launch_op(op, din, dout, n, h->want_status ? c->dstatus : NULL, si);
+    if (!err) err = pncxrt_event_record(c->sev_conv[e], si);
+    if (!err) err = pncxrt_stream_wait_event(so, c->sev_conv[e]);
+    if (!err && ev) err = pncxrt_event_record(ev[2], so);
+    if (!err) err = pncxrt_memcpy_d2h(dst, dout, (size_t)n * op->ds, so);
+    if (!err && ev) err = pncxrt_event_record(ev[3], so);
+    if (!err) err = pncxrt_event_record(c->sev_out[e], so);
+    PH_ADD(PH_CONV_ENQUEUE, t0);
+    if (err) {
+        h->err = err < 0 ? err : PNCX_EDEVICE;
+        return h->err;
+    }
+    h->pushed++;
+    return k;
+}
+
+/* chunk k's result is in its host destination */
+int pncx_stage_wait(pncx_stage *h, int k)
+{
+    int err;
+    double t0;
+    if (h->err) return h->err;
+    if (k < h->waited) return NC_NOERR;
+    if (k >= h->pushed || k < h->pushed - NSEV) return NC_EINVAL;
+    t0 = PH_T0();
+    err = pncxrt_event_sync(h->c->sev_out[k % NSEV]);
+    PH_ADD(PH_CONV_SYNC, t0);
+    if (err) return h->err = PNCX_EDEVICE;
+    h->waited = k + 1;
+    return NC_NOERR;
+}
+
+/* wait for every chunk, release the context; the call's first status */
+int pncx_stage_end(pncx_stage *h)
+{
+    ctx_t *c;
+    int err, st = 0, i;
+    double t0;
+    if (h == NULL) return NC_NOERR;
+    c = h->c;
+    err = h->err;
+    t0 = PH_T0();
+    for (i = 0; i < NSLOT; i++) {                  /* also drains after an error */
+        const int e2 = pncxrt_stream_sync(c->stream[i]);
+        if (!err && e2) err = PNCX_EDEVICE;
+    }
+    PH_ADD(PH_CONV_SYNC, t0);
+    for (i = 0; i < h->ph_ev && !err; i++) {
+        float a = 0, b = 0, d = 0;
+        void **ev = &c->pev[4 * i];
+        if (pncxrt_event_elapsed_ms(&a, ev[0], ev[1]) || pncxrt_event_elapsed_ms(&b, ev[1], ev[2]) ||
+            pncxrt_event_elapsed_ms(&d, ev[2], ev[3]))
+            break;
+        pncx_ph_add_us(PH_GPU_H2D, 1e3 * a);
+        pncx_ph_add_us(PH_GPU_KERNEL, 1e3 * b);
+        pncx_ph_add_us(PH_GPU_D2H, 1e3 * d);
+    }
+    t0 = PH_T0();
+    if (!err && h->want_status && h->pushed > 0) {  /* the status word, through pinned memory */
+        err = pncxrt_memcpy_d2h(c->hstat, c->dstatus, sizeof(int), c->stream[0]);
+        if (!err) err = pncxrt_stream_sync(c->stream[0]);
+        if (!err) st = c->hstat[0];
+    }
+    PH_ADD(PH_CONV_STATUS, t0);
+    t0 = PH_T0();
+    unpin_all(&h->pn);
+    PH_ADD(PH_CONV_UNPIN, t0);
+    pthread_mutex_unlock(&c->lock);
+    free(h);
+    if (err) return err < 0 ? err : PNCX_EDEVICE;
+    return st;
+}
+
+long long pncx_stage_chunk(const pncx_stage *h) { return h->chunk; }
+
+/* the whole call through a stage: host-buffer entry points */
 static int host_staged(const op_t *op, const void *src, void *dst, long long n, int preserve)
 {
-    ctx_t *c = get_ctx();
-    size_t per_elem, chunk_elems, cb;
-    long long off;
-    int slot, err = 0, st[NSLOT] = {0}, i, used;
-    /* a same-type swap cannot report NC_ERANGE: no status words to zero or
-     * read back (each costs a command and, for the read, a synchronise) */
-    const int want_status = op->kind != PNCXK_SWAP;
-    pinned_t pn = {{NULL, NULL}, 0};
-    if (c == NULL) return PNCX_EDEVICE;
-    pthread_mutex_lock(&c->lock);
-    pin_range(&pn, src, (size_t)n * op->ss);
-    pin_range(&pn, dst, (size_t)n * op->ds);
-    per_elem = (size_t)op->ss + (size_t)op->ds;
-    cb = chunk_bytes();
-    chunk_elems = cb / per_elem;
-    if (chunk_elems < 1) chunk_elems = 1;
-    if ((long long)chunk_elems > n) chunk_elems = (size_t)n;
-    err = ensure_dbuf(c, ALIGN16(chunk_elems * op->ss) + ALIGN16(chunk_elems * op->ds));
-    used = (long long)chunk_elems >= n ? 1 : NSLOT;            /* slots (streams) this call touches */
-    for (i = 0; i < used && want_status && !err; i++)
-        err = pncxrt_memset(c->dstatus + i, 0, sizeof(int), c->stream[i]);
-    for (off = 0, slot = 0; off < n && !err; off += (long long)chunk_elems, slot ^= 1) {
-        long long m = n - off < (long long)chunk_elems ? n - off : (long long)chunk_elems;
-        uint8_t *din = (uint8_t *)c->dbuf[slot];
-        uint8_t *dout = din + ALIGN16(chunk_elems * op->ss);
-        void *s = c->stream[slot];
-        const uint8_t *hs = (const uint8_t *)src + (size_t)off * op->ss;
-        uint8_t *hd = (uint8_t *)dst + (size_t)off * op->ds;
-        if (op->ss == op->ds && src == dst) dout = din;      /* in-place swap */
-        err = pncxrt_memcpy_h2d(din, hs, (size_t)m * op->ss, s);
-        if (!err && preserve && dout != din) err = pncxrt_memcpy_h2d(dout, hd, (size_t)m * op->ds, s);
-        if (!err) {
-            if (!(op->kind == PNCXK_SWAP && op->a == 1 && dout == din))
-                err = launch_op(op, din, dout, m, want_status ? c->dstatus + slot : NULL, s);
-        }
-        if (!err) err = pncxrt_memcpy_d2h(hd, dout, (size_t)m * op->ds, s);
+    pncx_stage *h;
+    long long off, chunk;
+    int err;
+    chunk = stage_chunk_elems(op, n);
+    if ((err = stage_open(&h, op, preserve, chunk)) != NC_NOERR) return err;
+    pin_range(&h->pn, src, (size_t)n * op->ss);
+    pin_range(&h->pn, dst, (size_t)n * op->ds);
+    for (off = 0; off < n; off += chunk) {
+        const long long m = n - off < chunk ? n - off : chunk;
+        const int k = pncx_stage_push(h, (const uint8_t *)src + (size_t)off * op->ss,
+                                      (uint8_t *)dst + (size_t)off * op->ds, m);
+        if (k < 0) break;
     }
-    for (i = 0; i < used; i++) {
-        int e2 = pncxrt_stream_sync(c->stream[i]);
-        if (!err && e2) err = e2;
-    }
-    /* both streams are done: the used status words in one copy */
-    if (!err && want_status) err = pncxrt_memcpy_d2h(st, c->dstatus, sizeof(int) * (size_t)used, c->stream[0]);
-    if (!err && want_status) err = pncxrt_stream_sync(c->stream[0]);
-    unpin_all(&pn);
-    pthread_mutex_unlock(&c->lock);
-    if (err) return err < 0 ? err : PNCX_EDEVICE;
-    for (i = 0; i < used; i++)
-        if (st[i] != 0) return st[i];
-    return NC_NOERR;
+    return pncx_stage_end(h);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -813,8 +1105,8 @@ struct pncx_dtype {
  * element.  PNCX_TOFF_MAX_ELEMS overrides (0 disables; read at commit). */
 static long long toff_max_elems(void)
 {
-    const char *e = getenv("PNCX_TOFF_MAX_ELEMS");
-    return e ? atoll(e) : (1LL << 26);
+    const long long v = pncx_knob(PNCXK_KNOB_TOFF_MAX_ELEMS);
+    return v >= 0 ? v : (1LL << 26);
 }
 
 int pncx_type_commit(int itype, pncx_offset nblocks, const pncx_offset *disp,
@@ -942,7 +1234,7 @@ int pncx_type_commit(int itype, pncx_offset nblocks, const pncx_offset *disp,
              * 32-bit base per chunk plus 16-bit offsets: 2 B of HBM per
              * element instead of 4 (PNCX_TOFF16=0 keeps 32 bits) */
             unsigned *o = (unsigned *)malloc(sizeof(unsigned) * (size_t)t->tn);
-            const char *e16 = getenv("PNCX_TOFF16");
+            const long long k16 = pncx_knob(PNCXK_KNOB_TOFF16);
             size_t bytes = sizeof(unsigned) * (size_t)t->tn;
             void *up = o;
             if (o == NULL) derr = NC_ENOMEM;
@@ -950,7 +1242,7 @@ int pncx_type_commit(int itype, pncx_offset nblocks, const pncx_offset *disp,
                 const long long ln = (i + 1 < k ? t->pre[i + 1] : t->tn) - t->pre[i];
                 for (e = 0; e < ln; e++) o[t->pre[i] + e] = (unsigned)(t->disp[i] - t->lo + e * isz);
             }
-            if (!derr && (e16 == NULL || atoi(e16) != 0)) {
+            if (!derr && k16 != 0) {
                 const long long nq16 = (t->tn + 63) / 64;
                 unsigned *base = (unsigned *)malloc(sizeof(unsigned) * (size_t)nq16 + sizeof(unsigned short) * (size_t)t->tn);
                 int fits = base != NULL;
@@ -1048,11 +1340,7 @@ static int flex_vec(const op_t *op)
 }
 
 /* PNCX_TMAP_IMAP=0 keeps lattice tables on the run-piece kernel (A/B) */
-static int tmap_imap_enabled(void)
-{
-    const char *e = getenv("PNCX_TMAP_IMAP");
-    return e == NULL || atoi(e) != 0;
-}
+static int tmap_imap_enabled(void) { return pncx_knob(PNCXK_KNOB_TMAP_IMAP) != 0; }
 
 /* vec: elements per 16-byte vector of the call's conversion (0: none);
  * *koff: bytes to add to the user pointer handed to the kernel */
@@ -1481,11 +1769,7 @@ static void batch_time(ctx_t *c)
  * two class kernels, in alternating runs on one box
  * (profiles/r03_fuse_ab.txt): the ramp and drain it saves are not where
  * the time goes.  Read per call, so tests can run both ways in one process. */
-static int batch_fuse_enabled(void)
-{
-    const char *e = getenv("PNCX_BATCH_FUSE");
-    return e != NULL && atoi(e) != 0;
-}
+static int batch_fuse_enabled(void) { return pncx_knob(PNCXK_KNOB_BATCH_FUSE) == 1; }
 
 /* launch the class kernels of a plan whose descriptors are on the device */
 static int launch_classes(const cls_t *cls, int ncls, uint8_t *dbase, size_t soff, size_t moff, int sval,

@@ -277,36 +277,16 @@ static void sink_release(hipStream_t) {
 }  // namespace pncx
 
 namespace pncx {
-int tile_u(int dflt) {     // read per launch: tests run both shapes in one process
-    const char *e = getenv("PNCX_TILE_U");
-    const int v = e != nullptr ? atoi(e) : dflt;
-    return v == 1 || v == 2 || v == 4 ? v : dflt;
+// A/B knobs: read once at load, pncx_knob_set in tests (pncx_shim.h)
+int tile_u(int dflt) {
+    const long long v = pncx_knob(PNCXK_KNOB_TILE_U);
+    return v == 1 || v == 2 || v == 4 ? (int)v : dflt;
 }
-
-int xpose_merge() {     // read per launch: tests run both tilings in one process
-    const char *e = getenv("PNCX_XPOSE_MERGE");
-    return e == nullptr || atoi(e) != 0;
-}
-
-int urun_enabled() {     // read per launch: tests run both paths in one process
-    const char *e = getenv("PNCX_URUN");
-    return e == nullptr || atoi(e) != 0;
-}
-
-int tmap_vec() {
-    const char *e = getenv("PNCX_TMAP_VEC");
-    return e == nullptr || atoi(e) != 0;
-}
-
-int imap_rows() {
-    const char *e = getenv("PNCX_IMAP_ROWS");
-    return e == nullptr || atoi(e) != 0;
-}
-
-int fuse_lanes() {     // read per launch, so tests can run both shapes in one process
-    const char *e = getenv("PNCX_FUSE_LANES");
-    return (e != nullptr && atoi(e) == 1024) ? 1024 : 256;
-}
+int xpose_merge() { return pncx_knob(PNCXK_KNOB_XPOSE_MERGE) != 0; }
+int urun_enabled() { return pncx_knob(PNCXK_KNOB_URUN) != 0; }
+int tmap_vec() { return pncx_knob(PNCXK_KNOB_TMAP_VEC) != 0; }
+int imap_rows() { return pncx_knob(PNCXK_KNOB_IMAP_ROWS) != 0; }
+int fuse_lanes() { return pncx_knob(PNCXK_KNOB_FUSE_LANES) == 1024 ? 1024 : 256; }
 }  // namespace pncx
 
 // single status word: any flag of this launch's epoch -> *status = sval
@@ -549,6 +529,9 @@ int pncxrt_stream_create(void **s) {
 int pncxrt_stream_destroy(void *s) { return s ? rt(hipStreamDestroy((hipStream_t)s), "hipStreamDestroy") : 0; }
 int pncxrt_stream_sync(void *s) { return rt(hipStreamSynchronize((hipStream_t)s), "hipStreamSynchronize"); }
 int pncxrt_event_create(void **e) { return rt(hipEventCreate((hipEvent_t *)e), "hipEventCreate"); }
+int pncxrt_event_create_fast(void **e) {
+    return rt(hipEventCreateWithFlags((hipEvent_t *)e, hipEventDisableTiming), "hipEventCreateWithFlags");
+}
 int pncxrt_event_destroy(void *e) { return e ? rt(hipEventDestroy((hipEvent_t)e), "hipEventDestroy") : 0; }
 int pncxrt_event_record(void *e, void *s) {
     return rt(hipEventRecord((hipEvent_t)e, (hipStream_t)s), "hipEventRecord");
@@ -579,12 +562,21 @@ int pncxrt_host_register(void *p, size_t n) {
     return PNCX_EDEVICE;
 }
 int pncxrt_host_unregister(void *p) { return rt(hipHostUnregister(p), "hipHostUnregister"); }
-int pncxrt_is_device_ptr(const void *p) {
+int pncxrt_ptr_device(const void *p) {
     hipPointerAttribute_t at;
-    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    if (p == nullptr || hipPointerGetAttributes(&at, p) != hipSuccess) {
         (void)hipGetLastError();
-        return 0;
+        return -1;
     }
-    return at.type == hipMemoryTypeDevice;
+    return at.type == hipMemoryTypeDevice ? at.device : -1;
+}
+int pncxrt_is_device_ptr(const void *p) {
+    /* device memory of the CURRENT device only: the kernels run there, and a
+     * buffer on another GPU would fault without peer access (the file layer
+     * refuses such a pointer: pncxrt_ptr_device) */
+    const int d = pncxrt_ptr_device(p);
+    int cur = -1;
+    if (d < 0 || hipGetDevice(&cur) != hipSuccess) return 0;
+    return d == cur;
 }
 }  // extern "C"

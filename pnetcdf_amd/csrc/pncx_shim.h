@@ -147,6 +147,27 @@ int pncxk_batch_map(const pncxk_batch_args *args);
  * hstat, then store seq into host-mapped *hdone (system scope) */
 int pncxk_batch_done(const int *dstat, int n, int *hstat, int *hdone, int seq, void *stream);
 
+/* ---- A/B knobs: read from the environment (PNCX_<name>) once when the
+ * library loads, changed by pncx_knob_set (include/pncx.h) in tests; -1 =
+ * not set, the code's own default applies ---- */
+enum {
+    PNCXK_KNOB_TILE_U,          /* k_tile_u tiles per block: 1, 2, 4         */
+    PNCXK_KNOB_XPOSE_MERGE,     /* 0: transposes tile dimension P alone      */
+    PNCXK_KNOB_URUN,            /* 0: uniform runs off k_urun                */
+    PNCXK_KNOB_TMAP_VEC,        /* 0: run pieces one element per lane        */
+    PNCXK_KNOB_IMAP_ROWS,       /* 0: varm rows off k_imap_rows              */
+    PNCXK_KNOB_FUSE_LANES,      /* 1024: fused batch with 1024-lane blocks   */
+    PNCXK_KNOB_BATCH_FUSE,      /* 1: fused two-class batch launch           */
+    PNCXK_KNOB_TMAP_IMAP,       /* 0: lattice tables stay run pieces         */
+    PNCXK_KNOB_TOFF16,          /* 0: 32-bit offset maps                     */
+    PNCXK_KNOB_TOFF_MAX_ELEMS,  /* largest short-run table given a map       */
+    PNCXK_KNOB_XPOSE_ORDER,     /* transpose tile order (0 row-major)        */
+    PNCXK_KNOB_TOFF_RUNS,       /* 0: short-run tables keep the offset map   */
+    PNCXK_KNOB_HOST_ZC,         /* 0: host-buffer calls stage through HBM    */
+    PNCXK_NKNOB
+};
+long long pncx_knob(int id);
+
 /* ---- HIP runtime wrappers (return 0 on success, PNCX_EDEVICE on error) ---- */
 int  pncxrt_device_count(void);
 int  pncxrt_set_device(int dev);
@@ -166,6 +187,7 @@ int  pncxrt_stream_create(void **s);
 int  pncxrt_stream_destroy(void *s);
 int  pncxrt_stream_sync(void *s);
 int  pncxrt_event_create(void **e);
+int  pncxrt_event_create_fast(void **e);   /* no timing: cheaper record and wait */
 int  pncxrt_event_destroy(void *e);
 int  pncxrt_event_record(void *e, void *stream);
 int  pncxrt_stream_wait_event(void *stream, void *e);
@@ -173,7 +195,8 @@ int  pncxrt_event_sync(void *e);
 /* 1 = done, 0 = not yet, PNCX_EDEVICE = error */
 int  pncxrt_event_query(void *e);
 int  pncxrt_event_elapsed_ms(float *ms, void *start, void *stop);
-int  pncxrt_is_device_ptr(const void *p);
+int  pncxrt_is_device_ptr(const void *p);   /* device memory of the current device */
+int  pncxrt_ptr_device(const void *p);      /* its device for device memory, else -1 */
 /* pin a pageable host range for DMA: 0 = registered by this call (caller
  * unregisters), 1 = already pinned/registered, PNCX_EDEVICE = could not */
 int  pncxrt_host_register(void *p, size_t n);

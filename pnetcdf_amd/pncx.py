@@ -73,6 +73,11 @@ def lib():
         "pncx_dev_status_read": (i, [vp, vp]),
         "pncx_strerror": (ctypes.c_char_p, [i]),
         "pncx_version": (ctypes.c_char_p, []),
+        "pncx_knob_set": (i, [ctypes.c_char_p, ll]),
+        "pncx_knob_get": (i, [ctypes.c_char_p, ctypes.POINTER(ll)]),
+        "pncx_phases": (i, [i]),
+        "pncx_phase_name": (ctypes.c_char_p, [i]),
+        "pncx_phase_read": (i, [i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ll)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -95,6 +100,36 @@ def version():
 
 def device_count():
     return lib().pncx_device_count()
+
+
+def knob_set(name, value):
+    """Set an A/B knob (pncx_knob_set; name as in PNCX_<name>, -1 = default)."""
+    _check(lib().pncx_knob_set(name.encode(), int(value)), f"knob_set {name}", (T.NC_NOERR,))
+
+
+def knob_get(name):
+    v = ctypes.c_longlong(0)
+    _check(lib().pncx_knob_get(name.encode(), ctypes.byref(v)), f"knob_get {name}", (T.NC_NOERR,))
+    return v.value
+
+
+def phases(enable):
+    """Turn per-phase timing of the host-buffer paths on (clearing it) or off."""
+    lib().pncx_phases(1 if enable else 0)
+
+
+def phase_sums():
+    """{phase name: (microseconds, count)} of the phases that ran."""
+    L, out, i = lib(), {}, 0
+    while True:
+        nm = L.pncx_phase_name(i)
+        if nm is None:
+            return out
+        us, n = ctypes.c_double(0), ctypes.c_longlong(0)
+        L.pncx_phase_read(i, ctypes.byref(us), ctypes.byref(n))
+        if n.value:
+            out[nm.decode()] = (us.value, n.value)
+        i += 1
 
 
 class Seg(ctypes.Structure):

@@ -26,3 +26,20 @@ def pncx():
     from pnetcdf_amd import pncx as P
     P.lib()
     return P
+
+
+@pytest.fixture
+def knob():
+    """knob(name, value): set an A/B switch of libpncx (pncx_knob_set, read
+    once from PNCX_<name> at load) for this test; restored afterwards."""
+    from pnetcdf_amd import pncx as P
+    saved = {}
+
+    def set_(name, value):
+        if name not in saved:
+            saved[name] = P.knob_get(name)
+        P.knob_set(name, int(value))
+
+    yield set_
+    for name, value in saved.items():
+        P.knob_set(name, value)

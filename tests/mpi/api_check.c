@@ -47,6 +47,8 @@
  *       define-mode only (dims, variables, text attributes) on N ranks: the
  *       header rank 0 writes must not depend on N.
  */
+#define _GNU_SOURCE
+#include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 #include <mpi.h>
 #include <stdint.h>
@@ -315,13 +317,50 @@ static int cmp_dbl(const void *a, const void *b)
     return x < y ? -1 : x > y;
 }
 
-/* config 1 timed (bench.py's c1 leg): one open file, reps puts then reps gets */
+/* per-phase sums of libpncx (pncx_phases, include/pncx.h), looked up at run
+ * time so this program links against libpnetcdf alone */
+static int phases_on(void)
+{
+    const char *e = getenv("PNCX_PHASES");
+    return e != NULL && atoi(e) != 0;
+}
+
+static void phases_reset(void)
+{
+    int (*on)(int) = (int (*)(int))dlsym(RTLD_DEFAULT, "pncx_phases");
+    if (on) on(1);
+}
+
+/* "label": {"phase": [us per call, runs per call], ...} for phases that ran */
+static void phases_print(const char *label, int calls)
+{
+    const char *(*name)(int) = (const char *(*)(int))dlsym(RTLD_DEFAULT, "pncx_phase_name");
+    int (*rd)(int, double *, long long *) = (int (*)(int, double *, long long *))dlsym(RTLD_DEFAULT, "pncx_phase_read");
+    int id, k = 0;
+    if (!name || !rd || calls <= 0) return;
+    printf(", \"%s\": {", label);
+    for (id = 0; name(id) != NULL; id++) {
+        double us = 0;
+        long long n = 0;
+        rd(id, &us, &n);
+        if (n == 0) continue;
+        printf("%s\"%s\": [%.2f, %.2f]", k++ ? ", " : "", name(id), us / calls, (double)n / calls);
+    }
+    printf("}");
+}
+
+/* config 1 timed (bench.py's c1 leg): one open file, reps puts then reps gets.
+ * With PNCX_PHASES=1 the line also carries the per-phase time of the calls
+ * after the first (put_phases / get_phases, us per call). */
 static int mode_c1bench(const char *path, MPI_Offset n, int reps, int dev)
 {
     int *h = (int *)malloc((size_t)n * 4), *g = (int *)calloc((size_t)n, 4), ncid, dimid, varid, r, bad = 0;
     double *tp = (double *)calloc((size_t)reps, sizeof(double)), *tg = (double *)calloc((size_t)reps, sizeof(double));
     void *dh = NULL, *dg = NULL;
     MPI_Offset start[1] = {0}, count[1] = {n}, off = 0, i;
+    double put_us[64] = {0};
+    long long put_n[64] = {0};
+    int phase_put_done = 0;
     for (i = 0; i < n; i++) h[i] = (int)((uint32_t)i * 2654435761u);
     if (dev) {
         dh = to_dev(h, (size_t)n * 4);
@@ -334,11 +373,21 @@ static int mode_c1bench(const char *path, MPI_Offset n, int reps, int dev)
     CHECK(ncmpi_inq_varoffset(ncid, varid, &off));
     for (r = 0; r < reps; r++) {
         const double t0 = MPI_Wtime();
+        if (r == 1 && phases_on()) phases_reset();
         CHECK(ncmpi_put_vara_int_all(ncid, varid, start, count, dev ? dh : (void *)h));
         tp[r] = MPI_Wtime() - t0;
     }
+    if (phases_on()) phase_put_done = 1;
+    if (phases_on()) {
+        /* keep the put sums for printing after the get loop */
+        const char *(*name)(int) = (const char *(*)(int))dlsym(RTLD_DEFAULT, "pncx_phase_name");
+        int (*rd)(int, double *, long long *) = (int (*)(int, double *, long long *))dlsym(RTLD_DEFAULT, "pncx_phase_read");
+        int id;
+        for (id = 0; name && rd && name(id) != NULL && id < 64; id++) rd(id, &put_us[id], &put_n[id]);
+    }
     for (r = 0; r < reps; r++) {
         const double t0 = MPI_Wtime();
+        if (r == 1 && phases_on()) phases_reset();
         CHECK(ncmpi_get_vara_int_all(ncid, varid, start, count, dev ? dg : (void *)g));
         tg[r] = MPI_Wtime() - t0;
     }
@@ -350,8 +399,20 @@ static int mode_c1bench(const char *path, MPI_Offset n, int reps, int dev)
     qsort(tg, (size_t)reps, sizeof(double), cmp_dbl);
     printf("{\"mode\": \"c1bench\", \"n\": %lld, \"reps\": %d, \"dev\": %d, \"var_offset\": %lld, "
            "\"put_ms_median\": %.5f, \"put_ms_min\": %.5f, \"get_ms_median\": %.5f, \"get_ms_min\": %.5f, "
-           "\"errors\": %d}\n", (long long)n, reps, dev, (long long)off, 1e3 * tp[reps / 2], 1e3 * tp[0],
+           "\"errors\": %d", (long long)n, reps, dev, (long long)off, 1e3 * tp[reps / 2], 1e3 * tp[0],
            1e3 * tg[reps / 2], 1e3 * tg[0], nerrs);
+    if (phase_put_done && reps > 1) {
+        const char *(*name)(int) = (const char *(*)(int))dlsym(RTLD_DEFAULT, "pncx_phase_name");
+        int id, k = 0;
+        printf(", \"put_phases\": {");
+        for (id = 0; name && name(id) != NULL && id < 64; id++)
+            if (put_n[id] > 0)
+                printf("%s\"%s\": [%.2f, %.2f]", k++ ? ", " : "", name(id), put_us[id] / (reps - 1),
+                       (double)put_n[id] / (reps - 1));
+        printf("}");
+        phases_print("get_phases", reps - 1);
+    }
+    printf("}\n");
     if (dev) { hipFree(dh); hipFree(dg); }
     free(h); free(g); free(tp); free(tg);
     return nerrs != 0;

@@ -152,11 +152,11 @@ def test_flex_large_table(torch_cuda, where):
 
 
 @pytest.mark.parametrize("where", ["host", "dev"])
-def test_flex_table_search_path(torch_cuda, where, monkeypatch):
+def test_flex_table_search_path(torch_cuda, where, knob):
     """short-run tables normally get a per-element offset map at commit
     (tmode 4); with the map disabled the same cases take the chunk-indexed
     table search (tmode 2)"""
-    monkeypatch.setenv("PNCX_TOFF_MAX_ELEMS", "0")
+    knob("TOFF_MAX_ELEMS", "0")
     for tname, disp, blen, ext, bufcount, layout in TYPES:
         if layout == 2:
             dt = run_case(torch_cuda, where, T.NC_SHORT, T.ITYPE_INT, disp, blen, ext, bufcount, None, None,
@@ -175,13 +175,13 @@ def test_flex_table_search_path(torch_cuda, where, monkeypatch):
 @pytest.mark.parametrize("where", ["host", "dev"])
 @pytest.mark.parametrize("map16", ["1", "0"])
 @pytest.mark.parametrize("gap", [5, 3000])
-def test_flex_offset_map_widths(torch_cuda, where, map16, gap, monkeypatch):
+def test_flex_offset_map_widths(torch_cuda, where, map16, gap, knob):
     """short-run tables get a 16-bit offset map (a base per 64-element chunk,
     tmode 5) when every chunk spans under 64 KiB, else the 32-bit map (tmode
     4); PNCX_TOFF16=0 forces 32 bits.  Gaps of up to 3000 elements make
     chunks span ~1.5 MiB of doubles (32-bit map by necessity); partial last
     chunk and several copies included."""
-    monkeypatch.setenv("PNCX_TOFF16", map16)
+    knob("TOFF16", map16)
     rng = np.random.default_rng(gap + int(map16))
     nb = 5000
     blen = rng.integers(1, 8, nb)
@@ -269,12 +269,12 @@ def test_flex_short_runs_many_steps(torch_cuda, xt, it):
 @pytest.mark.parametrize("xt,it", [(T.NC_DOUBLE, T.ITYPE_DOUBLE), (T.NC_FLOAT, T.ITYPE_DOUBLE),
                                    (T.NC_SHORT, T.ITYPE_INT), (T.NC_INT, T.ITYPE_SHORT)])
 @pytest.mark.parametrize("where", ["host", "dev"])
-def test_flex_uniform_vector_runs(torch_cuda, where, xt, it, blen, gap, urun, monkeypatch):
+def test_flex_uniform_vector_runs(torch_cuda, where, xt, it, blen, gap, urun, knob):
     """uniform runs whose lengths hold whole 16-byte vectors, 16-byte aligned,
     over a contiguous count: one vector per lane (k_urun; PNCX_URUN=0 takes
     k_imap / k_tmap_runs).  blen 3 does not divide into vectors and falls
     back either way.  3 copies, NC_ERANGE from int -> NC_SHORT."""
-    monkeypatch.setenv("PNCX_URUN", urun)
+    knob("URUN", urun)
     nb = 4096 if blen <= 64 else 64
     disp = (np.arange(nb) * (blen + gap)).tolist()
     dt = run_case(torch_cuda, where, xt, it, disp, [blen] * nb, nb * (blen + gap), 3, None, None, 40 + blen)
@@ -286,12 +286,12 @@ def test_flex_uniform_vector_runs(torch_cuda, where, xt, it, blen, gap, urun, mo
                                    (T.NC_FLOAT, T.ITYPE_FLOAT), (T.NC_BYTE, T.ITYPE_UCHAR)])
 @pytest.mark.parametrize("where", ["host", "dev"])
 @pytest.mark.parametrize("ghost", [1, 2])
-def test_flex_lattice_subarray(torch_cuda, where, xt, it, tmap_imap, ghost, monkeypatch):
+def test_flex_lattice_subarray(torch_cuda, where, xt, it, tmap_imap, ghost, knob):
     """a 3-D subarray buftype (interior of a ghosted block: equal runs on a
     2-level lattice) x 2 copies: with PNCX_TMAP_IMAP=1 (default) it runs as a
     4-D varm over the first run (k_imap_rows) when its rows hold whole
     vectors, else through the run-piece kernel; both against numpy + oracle"""
-    monkeypatch.setenv("PNCX_TMAP_IMAP", tmap_imap)
+    knob("TMAP_IMAP", tmap_imap)
     L = (9, 10, 12)
     z, y = np.meshgrid(np.arange(L[0] - 2 * ghost), np.arange(L[1] - 2 * ghost), indexing="ij")
     disp = (((z + ghost) * L[1] * L[2] + (y + ghost) * L[2] + ghost)).reshape(-1).tolist()

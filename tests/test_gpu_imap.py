@@ -164,11 +164,11 @@ MERGE_CASES = [
 @pytest.mark.parametrize("count,imap", MERGE_CASES)
 @pytest.mark.parametrize("xt,it", [(T.NC_INT, T.ITYPE_DOUBLE), (T.NC_DOUBLE, T.ITYPE_DOUBLE), (T.NC_UINT64, T.ITYPE_SCHAR)])
 @pytest.mark.parametrize("merge", ["1", "0"])
-def test_imap_tile_merged_dims(torch_cuda, count, imap, xt, it, merge, monkeypatch):
+def test_imap_tile_merged_dims(torch_cuda, count, imap, xt, it, merge, knob):
     """k_imap_tile with the last two dimensions tiled as one virtual row
     (default) and tiled P alone (PNCX_XPOSE_MERGE=0): put and get against a
     numpy gather/scatter + the oracle, on device buffers."""
-    monkeypatch.setenv("PNCX_XPOSE_MERGE", merge)
+    knob("XPOSE_MERGE", merge)
     test_imap_put_get(torch_cuda, count, imap, xt, it, "dev")
 
 
@@ -187,10 +187,10 @@ ROW_CASES = [
 @pytest.mark.parametrize("xt,it", [(T.NC_DOUBLE, T.ITYPE_DOUBLE), (T.NC_INT, T.ITYPE_DOUBLE), (T.NC_SHORT, T.ITYPE_INT),
                                    (T.NC_BYTE, T.ITYPE_UCHAR), (T.NC_FLOAT, T.ITYPE_FLOAT)])
 @pytest.mark.parametrize("rows", ["1", "0"])
-def test_imap_contiguous_rows(torch_cuda, count, imap, xt, it, rows, monkeypatch):
+def test_imap_contiguous_rows(torch_cuda, count, imap, xt, it, rows, knob):
     """varm rows contiguous in the user buffer, a vector per lane
     (PNCX_IMAP_ROWS=1, default) or an element per lane (0): put and get
     against a numpy gather/scatter + the oracle, host and device buffers"""
-    monkeypatch.setenv("PNCX_IMAP_ROWS", rows)
+    knob("IMAP_ROWS", rows)
     for where in ("host", "dev"):
         test_imap_put_get(torch_cuda, count, imap, xt, it, where)

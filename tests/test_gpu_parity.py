@@ -90,12 +90,12 @@ def test_random_bits_vs_oracle(conv, xt):
 
 
 @pytest.mark.parametrize("u", [1, 2, 4])
-def test_tiles_per_block_vs_oracle(torch_cuda, u, monkeypatch):
+def test_tiles_per_block_vs_oracle(torch_cuda, u, knob):
     """The direct-shape kernels with 1, 2 or 4 tiles per block (k_tile /
     k_tile_u, PNCX_TILE_U; the default is 2 for the 2:1 widening tiles and 1
     otherwise): every pair both ways on random bits, with tile counts that
     are not multiples of u and scalar tails."""
-    monkeypatch.setenv("PNCX_TILE_U", str(u))
+    knob("TILE_U", str(u))
     dev, ora = HipDevConv(), OracleConv()
     rng = np.random.default_rng(0x711E + u)
     for xt in T.NUMERIC_XTYPES:
@@ -819,7 +819,7 @@ FUSE_CLASSES = [(T.PNCX_PUT, T.NC_SHORT, T.ITYPE_FLOAT), (T.PNCX_GET, T.NC_INT, 
                          f"{T.XNAME[c[1]]}_{T.INAME[c[2]]}")
 @pytest.mark.parametrize("seed", [1, 2])
 @pytest.mark.parametrize("lanes", [256, 1024])
-def test_dev_batch_fused_two_classes(torch_cuda, cls, seed, lanes, monkeypatch):
+def test_dev_batch_fused_two_classes(torch_cuda, cls, seed, lanes, knob):
     """With PNCX_BATCH_FUSE=1 (off by default: no faster) a batch
     of exactly one conversion class and same-type swaps runs as ONE fused
     launch (k_batch_fused: 256-lane blocks of one conversion tile or
@@ -829,8 +829,8 @@ def test_dev_batch_fused_two_classes(torch_cuda, cls, seed, lanes, monkeypatch):
     synchronous (twice, the second from the plan cache) and asynchronous."""
     torch = torch_cuda
     from pnetcdf_amd import pncx
-    monkeypatch.setenv("PNCX_BATCH_FUSE", "1")
-    monkeypatch.setenv("PNCX_FUSE_LANES", str(lanes))
+    knob("BATCH_FUSE", "1")
+    knob("FUSE_LANES", str(lanes))
     ora = OracleConv()
     rng = np.random.default_rng(0xF05E + seed)
     d, xt, it = cls

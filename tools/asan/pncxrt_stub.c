@@ -25,6 +25,7 @@ int pncxrt_stream_create(void **s) { (void)s; return NODEV; }
 int pncxrt_stream_destroy(void *s) { (void)s; return 0; }
 int pncxrt_stream_sync(void *s) { (void)s; return NODEV; }
 int pncxrt_event_create(void **e) { (void)e; return NODEV; }
+int pncxrt_event_create_fast(void **e) { (void)e; return NODEV; }
 int pncxrt_event_destroy(void *e) { (void)e; return 0; }
 int pncxrt_event_record(void *e, void *s) { (void)e; (void)s; return NODEV; }
 int pncxrt_stream_wait_event(void *s, void *e) { (void)e; (void)s; return NODEV; }
@@ -32,6 +33,7 @@ int pncxrt_event_sync(void *e) { (void)e; return NODEV; }
 int pncxrt_event_query(void *e) { (void)e; return NODEV; }
 int pncxrt_event_elapsed_ms(float *ms, void *a, void *b) { (void)ms; (void)a; (void)b; return NODEV; }
 int pncxrt_is_device_ptr(const void *p) { (void)p; return 0; }
+int pncxrt_ptr_device(const void *p) { (void)p; return -1; }
 int pncxrt_host_register(void *p, size_t n) { (void)p; (void)n; return NODEV; }
 int pncxrt_host_unregister(void *p) { (void)p; return 0; }
 const char *pncxrt_last_error(void) { return "no device (host-only ASan build)"; }
