@@ -337,9 +337,11 @@ int pncx_dev_batch_kernel_ms(double *total_ms, long long *calls);
  * PNCX_PHASES=1 in the environment.  pncx_phases(1) clears the sums and
  * turns recording on, pncx_phases(0) turns it off.  Phase ids run from 0
  * while pncx_phase_name(id) is not NULL; a phase's host time is summed in
- * microseconds with the number of times it ran.  Phases named "gpu.*" are
- * HIP-event intervals on the device (H2D, kernel, D2H), the others host
- * clock intervals. */
+ * microseconds with the number of times it ran.  The phases are host
+ * clock intervals; with pncx_phases(2) (PNCX_PHASES=2) the first chunks of
+ * a staged conversion also get HIP events, summed as "gpu.h2d", "gpu.kernel"
+ * and "gpu.d2h" (they serialise the pipeline a little: use them to see
+ * the device side, not to time the call). */
 int pncx_phases(int enable);
 /* A/B switches of the kernel and staging choices (DESIGN.md names each):
  * PNCX_<name> in the environment is read once when the library loads; this

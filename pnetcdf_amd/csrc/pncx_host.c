@@ -100,12 +100,12 @@ static const char *const g_ph_names[PH_N] = {
     "put.plan", "put.register", "put.convert", "put.write", "put.wait", "put.unregister", "put.total",
     "get.plan", "get.register", "get.read", "get.convert", "get.unregister", "get.total",
     "conv.lock_pin", "conv.enqueue", "conv.sync", "conv.status", "conv.unpin",
-    "gpu.h2d", "gpu.kernel", "gpu.d2h"};
+    "gpu.h2d", "gpu.kernel", "gpu.d2h", "file.window_map", "file.window_use"};
 
 /* A/B knobs (pncx_shim.h): the environment once at load, then pncx_knob_set */
 static const char *const g_knob_names[PNCXK_NKNOB] = {
     "TILE_U", "XPOSE_MERGE", "URUN", "TMAP_VEC", "IMAP_ROWS", "FUSE_LANES", "BATCH_FUSE", "TMAP_IMAP",
-    "TOFF16", "TOFF_MAX_ELEMS", "XPOSE_ORDER", "TOFF_RUNS", "HOST_ZC"};
+    "TOFF16", "TOFF_MAX_ELEMS", "XPOSE_ORDER", "TOFF_RUNS", "HOST_ZC", "IO_INLINE_MB", "FILE_WINDOW"};
 static long long g_knob[PNCXK_NKNOB];
 
 long long pncx_knob(int id)
@@ -144,7 +144,7 @@ __attribute__((constructor)) static void ph_init(void)
     const char *e = getenv("PNCX_PHASES");
     char nm[64];
     int i;
-    pncx_ph_on = e != NULL && atoi(e) != 0;
+    pncx_ph_on = e != NULL ? (atoi(e) < 0 ? 0 : atoi(e) > 2 ? 2 : atoi(e)) : 0;
     for (i = 0; i < PNCXK_NKNOB; i++) {
         snprintf(nm, sizeof nm, "PNCX_%s", g_knob_names[i]);
         e = getenv(nm);
@@ -176,7 +176,7 @@ int pncx_phases(int enable)
         memset(g_ph_us, 0, sizeof g_ph_us);
         memset(g_ph_n, 0, sizeof g_ph_n);
     }
-    pncx_ph_on = enable != 0;
+    pncx_ph_on = enable < 0 ? 0 : enable > 2 ? 2 : enable;
     pthread_mutex_unlock(&g_ph_lock);
     return NC_NOERR;
 }
@@ -428,7 +428,7 @@ typedef struct ctx_t {
      * event per chunk after its kernel and after its D2H, a pinned status word */
     void  *sdbuf[4];
     size_t sdbuf_size;
-    void  *sev_conv[32], *sev_out[32];
+    void  *sev_conv[32], *sev_out[32], *sev_init;
     int   *hstat;
 } ctx_t;
 
@@ -563,9 +563,21 @@ static void unpin_all(pinned_t *pn)
  */
 #define NDBUF 4
 #define NSEV 32                     /* chunks in flight (event ring)       */
+/* How a chunk crosses PCIe (PNCX_HOST_ZC knob; tools/c1_probe.hip on MI355X,
+ * 4 MiB 4-byte swap, profiles/r04d_c1_probe_4m.txt):
+ *   STAGE_COPY  H2D (SDMA), kernel in HBM, D2H (SDMA)        1 chunk 185 us
+ *   STAGE_ZCOUT H2D (SDMA), kernel stores to the host        4 chunks: 68 us to
+ *               destination directly (zero-copy stores)      the first, 178 all
+ *   STAGE_ZC    the kernel loads from and stores to host     2 chunks 149 us
+ *               memory (no SDMA)
+ * The zero-copy modes need a host destination (and for STAGE_ZC a source)
+ * that is pinned or registered; otherwise the chunk is copied. */
+enum { STAGE_COPY = 0, STAGE_ZCOUT = 1, STAGE_ZC = 2 };
+
 struct pncx_stage {
     ctx_t *c;
     op_t op;
+    int mode;
     int preserve, want_status;
     long long chunk;                /* elements per device slot            */
     size_t din_bytes;               /* input part of a slot                */
@@ -578,12 +590,14 @@ struct pncx_stage {
 static int stage_slots(ctx_t *c, size_t slot_bytes)
 {
     int i;
-    if (c->sev_out[NSEV - 1] == NULL)
+    if (c->sev_init == NULL) {
         for (i = 0; i < NSEV; i++)
             if (pncxrt_event_create_fast(&c->sev_conv[i]) || pncxrt_event_create_fast(&c->sev_out[i]))
                 return PNCX_EDEVICE;
+        if (pncxrt_event_create_fast(&c->sev_init)) return PNCX_EDEVICE;
+    }
     if (c->hstat == NULL && pncxrt_host_alloc((void **)&c->hstat, 64) != 0) return PNCX_EDEVICE;
-    if (c->sdbuf_size >= slot_bytes) return 0;
+    if (c->sdbuf_size >= slot_bytes || slot_bytes == 0) return 0;
     for (i = 0; i < NSLOT; i++) pncxrt_stream_sync(c->stream[i]);
     for (i = 0; i < NDBUF; i++) {
         pncxrt_free(c->sdbuf[i]);
@@ -625,9 +639,19 @@ static int stage_open(pncx_stage **hp, const op_t *op, int preserve, long long m
     h->want_status = op->kind != PNCXK_SWAP;
     h->chunk = max_chunk > 0 ? max_chunk : 1;
     h->din_bytes = ALIGN16((size_t)h->chunk * (size_t)op->ss);
+    {
+        const long long m = pncx_knob(PNCXK_KNOB_HOST_ZC);
+        h->mode = m < 0 ? STAGE_ZCOUT : (int)m;
+        if (h->mode > STAGE_ZC) h->mode = STAGE_COPY;
+    }
     pthread_mutex_lock(&c->lock);
     err = stage_slots(c, h->din_bytes + ALIGN16((size_t)h->chunk * (size_t)op->ds));
-    if (!err && h->want_status) err = pncxrt_memset(c->dstatus, 0, sizeof(int), c->stream[0]);
+    if (!err && h->want_status) {
+        /* both streams' kernels may set the word: zero it before either runs */
+        err = pncxrt_memset(c->dstatus, 0, sizeof(int), c->stream[0]);
+        if (!err) err = pncxrt_event_record(c->sev_init, c->stream[0]);
+        if (!err) err = pncxrt_stream_wait_event(c->stream[1], c->sev_init);
+    }
     if (!err && pncx_ph_on && c->pev[0] == NULL) {
         int i;
         for (i = 0; i < 4 * PH_EVCH; i++)
@@ -679,7 +703,38 @@ int pncx_stage_push(pncx_stage *h, const void *src, void *dst, long long n)
     if (k - h->waited >= NSEV) {                   /* the event ring is full: wait the oldest */
         if ((err = pncx_stage_wait(h, k - NSEV)) != NC_NOERR) return err;
     }
-    if (pncx_ph_on && c->pev[4 * PH_EVCH - 1] && h->ph_ev < PH_EVCH) ev = &c->pev[4 * h->ph_ev++];
+    if (pncx_ph_on > 1 && c->pev[4 * PH_EVCH - 1] && h->ph_ev < PH_EVCH) ev = &c->pev[4 * h->ph_ev++];
+    if (h->mode != STAGE_COPY && !(op->kind == PNCXK_SWAP && op->a == 1)) {
+        /* zero-copy: the kernel writes the host destination itself */
+        void *ddst = pncxrt_host_dptr(dst);
+        const void *dsrc = h->mode == STAGE_ZC ? pncxrt_host_dptr(src) : NULL;
+        if (ddst != NULL && h->mode == STAGE_ZC && dsrc != NULL) {
+            void *q = c->stream[k & 1];
+            if (!err) err = launch_op(op, dsrc, ddst, n, h->want_status ? c->dstatus : NULL, q);
+            if (!err) err = pncxrt_event_record(c->sev_out[e], q);
+            PH_ADD(PH_CONV_ENQUEUE, t0);
+            if (err) return h->err = err < 0 ? err : PNCX_EDEVICE;
+            h->pushed++;
+            return k;
+        }
+        if (ddst != NULL) {
+            /* the slot's last reader is chunk k-NDBUF's kernel, on the out stream */
+            if (k >= NDBUF) err = pncxrt_stream_wait_event(si, c->sev_out[(k - NDBUF) % NSEV]);
+            if (!err && ev) err = pncxrt_event_record(ev[0], si);
+            if (!err) err = pncxrt_memcpy_h2d(din, src, (size_t)n * op->ss, si);
+            if (!err && ev) err = pncxrt_event_record(ev[1], si);
+            if (!err) err = pncxrt_event_record(c->sev_conv[e], si);
+            if (!err) err = pncxrt_stream_wait_event(so, c->sev_conv[e]);
+            if (!err && ev) err = pncxrt_event_record(ev[2], so);
+            if (!err) err = launch_op(op, din, ddst, n, h->want_status ? c->dstatus : NULL, so);
+            if (!err && ev) err = pncxrt_event_record(ev[3], so);
+            if (!err) err = pncxrt_event_record(c->sev_out[e], so);
+            PH_ADD(PH_CONV_ENQUEUE, t0);
+            if (err) return h->err = err < 0 ? err : PNCX_EDEVICE;
+            h->pushed++;
+            return k;
+        }
+    }
     if (op->ss == op->ds && src == dst) dout = din;            /* in-place swap */
     /* the slot's previous chunk must be back on the host */
     if (k >= NDBUF) err = pncxrt_stream_wait_event(si, c->sev_out[(k - NDBUF) % NSEV]);
@@ -762,6 +817,39 @@ int pncx_stage_end(pncx_stage *h)
 }
 
 long long pncx_stage_chunk(const pncx_stage *h) { return h->chunk; }
+
+/* One conversion launch between device-accessible pointers (HBM, pinned or
+ * registered host memory, a registered file window), waited for.  Returns
+ * the status (NC_ERANGE) or an error. */
+int pncx_direct_convert(int dir, int cdf_ver, int xtype, int itype, const void *fillp, const void *dsrc,
+                        void *ddst, long long n)
+{
+    op_t op;
+    ctx_t *c;
+    int err, st = 0, want;
+    double t0 = PH_T0();
+    if (dir == PNCX_SWAP_DIR) {
+        memset(&op, 0, sizeof op);
+        op.kind = PNCXK_SWAP;
+        op.a = op.ss = op.ds = xtype;
+    } else if ((err = classify(dir, cdf_ver, xtype, itype, fillp, &op)) != NC_NOERR) {
+        return err;
+    }
+    if (n <= 0) return NC_NOERR;
+    if (!have_device() || (c = get_ctx()) == NULL) return PNCX_EDEVICE;
+    want = op.kind != PNCXK_SWAP;
+    pthread_mutex_lock(&c->lock);
+    err = stage_slots(c, 0);                      /* the events and the pinned status word */
+    if (!err && want) err = pncxrt_memset(c->dstatus, 0, sizeof(int), c->stream[0]);
+    if (!err) err = launch_op(&op, dsrc, ddst, n, want ? c->dstatus : NULL, c->stream[0]);
+    if (!err && want) err = pncxrt_memcpy_d2h(c->hstat, c->dstatus, sizeof(int), c->stream[0]);
+    if (!err) err = pncxrt_stream_sync(c->stream[0]);
+    if (!err && want) st = c->hstat[0];
+    pthread_mutex_unlock(&c->lock);
+    PH_ADD(dir == PNCX_GET ? PH_GET_CONVERT : PH_PUT_CONVERT, t0);
+    if (err) return err < 0 ? err : PNCX_EDEVICE;
+    return st;
+}
 
 /* the whole call through a stage: host-buffer entry points */
 static int host_staged(const op_t *op, const void *src, void *dst, long long n, int preserve)

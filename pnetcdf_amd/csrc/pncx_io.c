@@ -343,6 +343,14 @@ int pio_wait(pio_batch *b)
     return err;
 }
 
+int pio_rw_inline(int fd, int write, const pio_run *runs, size_t n)
+{
+    long long total = 0;
+    size_t i;
+    for (i = 0; i < n; i++) total += runs[i].len;
+    return total == 0 ? NC_NOERR : do_range(fd, write ? 1 : 0, runs, n, 0, total);
+}
+
 int pio_rw(int fd, int write, const pio_run *runs, size_t n)
 {
     pio_batch b;

@@ -36,6 +36,8 @@ void pio_batch_destroy(pio_batch *b);
 int  pio_submit(pio_batch *b, int fd, int write, const pio_run *runs, size_t n);
 /* Wait for every job submitted on b; returns the first error (NC_EWRITE/NC_EREAD). */
 int  pio_wait(pio_batch *b);
+/* The job on the calling thread with pread/pwrite (no pool, no mapping). */
+int  pio_rw_inline(int fd, int write, const pio_run *runs, size_t n);
 /* Synchronous convenience: submit + wait. */
 int  pio_rw(int fd, int write, const pio_run *runs, size_t n);
 int  pio_threads(void);

@@ -179,10 +179,21 @@ bool same_owner(const FlagSlot *c, int dev, hipStream_t st, pthread_t self) {
     return c->live && c->dev == dev && c->stream == st && (st != hipStreamPerThread || pthread_equal(c->thread, self));
 }
 
-// queue an array for freeing once the mutex is dropped (caller holds it);
-// with the list full the array is leaked rather than freed under the mutex
+// queue an array for freeing once the mutex is dropped (caller holds it).
+// Every release frees the list, and one acquire retires at most two arrays,
+// so the list cannot fill up; if it ever did, the array is freed here, under
+// the mutex (hipFree drains the device first, so no queued kernel or reduce
+// still reads it) rather than leaked.
 void retire(int dev, int *flags) {
-    if (flags == nullptr || g_nretired >= NRETIRE) return;
+    if (flags == nullptr) return;
+    if (g_nretired >= NRETIRE) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        if (dev != cur) (void)hipSetDevice(dev);
+        (void)hipFree(flags);
+        if (dev != cur) (void)hipSetDevice(cur);
+        return;
+    }
     g_retired[g_nretired++] = Retired{dev, flags};
 }
 
@@ -557,11 +568,35 @@ int pncxrt_host_register(void *p, size_t n) {
         (at.type == hipMemoryTypeHost || at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged))
         return 1;
     (void)hipGetLastError();
-    if (hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess) return 0;
+    if (hipHostRegister(p, n, hipHostRegisterMapped) == hipSuccess) return 0;
     (void)hipGetLastError();
     return PNCX_EDEVICE;
 }
 int pncxrt_host_unregister(void *p) { return rt(hipHostUnregister(p), "hipHostUnregister"); }
+int pncxrt_host_register_map(void *p, size_t n, int readonly) {
+    unsigned fl = hipHostRegisterMapped | (readonly ? hipHostRegisterReadOnly : 0u);
+    if (hipHostRegister(p, n, fl) == hipSuccess) return 0;
+    (void)hipGetLastError();
+    if (readonly && hipHostRegister(p, n, hipHostRegisterMapped) == hipSuccess) return 0;
+    (void)hipGetLastError();
+    return PNCX_EDEVICE;
+}
+void *pncxrt_host_dptr(const void *p) {
+    /* the device address of pinned or registered host memory (the kernels
+     * read and write it over PCIe), NULL for pageable or device memory */
+    hipPointerAttribute_t at;
+    void *d = nullptr;
+    if (p == nullptr || hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (at.type != hipMemoryTypeHost) return nullptr;
+    if (hipHostGetDevicePointer(&d, (void *)p, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return d;
+}
 int pncxrt_ptr_device(const void *p) {
     hipPointerAttribute_t at;
     if (p == nullptr || hipPointerGetAttributes(&at, p) != hipSuccess) {

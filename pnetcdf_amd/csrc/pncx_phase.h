@@ -32,6 +32,8 @@ enum {
     PH_GPU_H2D,         /* HIP-event intervals on the device               */
     PH_GPU_KERNEL,
     PH_GPU_D2H,
+    PH_WIN_MAP,         /* a file window mapped and registered             */
+    PH_WIN_USE,         /* a request converted through a file window       */
     PH_N
 };
 

@@ -163,7 +163,10 @@ enum {
     PNCXK_KNOB_TOFF_MAX_ELEMS,  /* largest short-run table given a map       */
     PNCXK_KNOB_XPOSE_ORDER,     /* transpose tile order (0 row-major)        */
     PNCXK_KNOB_TOFF_RUNS,       /* 0: short-run tables keep the offset map   */
-    PNCXK_KNOB_HOST_ZC,         /* 0: host-buffer calls stage through HBM    */
+    PNCXK_KNOB_HOST_ZC,         /* host-buffer chunks: 0 copy, 1 zero-copy
+                                 * stores (default), 2 zero-copy both ways   */
+    PNCXK_KNOB_IO_INLINE_MB,    /* requests below: I/O on the calling thread */
+    PNCXK_KNOB_FILE_WINDOW,     /* tmpfs file windows: 0 off, 2 at first use */
     PNCXK_NKNOB
 };
 long long pncx_knob(int id);
@@ -201,6 +204,11 @@ int  pncxrt_ptr_device(const void *p);      /* its device for device memory, els
  * unregisters), 1 = already pinned/registered, PNCX_EDEVICE = could not */
 int  pncxrt_host_register(void *p, size_t n);
 int  pncxrt_host_unregister(void *p);
+/* device address of pinned/registered host memory, NULL otherwise */
+void *pncxrt_host_dptr(const void *p);
+/* register a shared file mapping for device access (read-only or not):
+ * 0 = registered, PNCX_EDEVICE = refused */
+int  pncxrt_host_register_map(void *p, size_t n, int readonly);
 /* host buffers at least this large are pinned for a call (pncx_host.c) */
 size_t pncxrt_pin_threshold(void);
 const char *pncxrt_last_error(void);

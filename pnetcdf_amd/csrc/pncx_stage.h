@@ -33,6 +33,12 @@ int pncx_stage_wait(pncx_stage *h, int k);
 int pncx_stage_end(pncx_stage *h);
 long long pncx_stage_chunk(const pncx_stage *h);
 
+/* one conversion launch between device-accessible pointers (HBM, pinned or
+ * registered host memory, a registered file window), waited for: the
+ * status (NC_ERANGE) or an error */
+int pncx_direct_convert(int dir, int cdf_ver, int xtype, int itype, const void *fillp, const void *dsrc,
+                        void *ddst, long long nelems);
+
 #ifdef __cplusplus
 }
 #endif

@@ -597,6 +597,114 @@ int main(int argc, char **argv) {
         t[r] = now_us() - a;
     }
     report("pread_into_pageable", t);
+    // ---- the GPU writing/reading the file's page cache directly: a shared
+    // mapping of the tmpfs file registered with HIP (zero-copy stores into
+    // the file pages; no CPU copy of the converted bytes)
+    {
+        const off_t base = 0;                       /* the variable begins at off = 512 */
+        const size_t span = (size_t)off + bytes;
+        bool ok = true;
+        std::vector<double> tm(reps), tr(reps), tk(reps), tu(reps);
+        CK(hipHostRegister(user, bytes, hipHostRegisterMapped));
+        void *duser = nullptr;
+        CK(hipHostGetDevicePointer(&duser, user, 0));
+        for (int r = 0; r < reps && ok; r++) {
+            double a = now_us();
+            unsigned char *m = (unsigned char *)mmap(NULL, span, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd, base);
+            if (m == MAP_FAILED) { perror("mmap"); ok = false; break; }
+            double b = now_us();
+            hipError_t e = hipHostRegister(m, span, hipHostRegisterMapped);
+            if (e != hipSuccess) { printf("# file mapping register failed: %s\n", hipGetErrorString(e)); (void)hipGetLastError(); munmap(m, span); ok = false; break; }
+            void *dm = nullptr;
+            CK(hipHostGetDevicePointer(&dm, m, 0));
+            double c = now_us();
+            hipLaunchKernelGGL(k_swap4, dim3(grid), dim3(256), 0, s, (const uint4 *)duser, (uint4 *)((char *)dm + off), (long long)nv);
+            CK(hipStreamSynchronize(s));
+            double d = now_us();
+            CK(hipHostUnregister(m));
+            munmap(m, span);
+            double e2 = now_us();
+            t[r] = e2 - a; tm[r] = b - a; tr[r] = c - b; tk[r] = d - c; tu[r] = e2 - d;
+        }
+        if (ok) {
+            report("fileput_zc.total(map+reg+kernel+unreg+unmap)", t);
+            report("fileput_zc.mmap_populate", tm);
+            report("fileput_zc.register", tr);
+            report("fileput_zc.kernel_user_to_filepages", tk);
+            report("fileput_zc.unregister_unmap", tu);
+            std::vector<uint32_t> chk(bytes / 4);
+            if (pread(fd, chk.data(), bytes, off) != (ssize_t)bytes) return 2;
+            for (size_t i = 0; i < bytes / 4; i++)
+                if (chk[i] != __builtin_bswap32(user[i])) { fprintf(stderr, "fileput mismatch at %zu\n", i); return 3; }
+            printf("# fileput_zc verified\n");
+            // persistent mapping: map + register once, the kernel per call
+            unsigned char *m = (unsigned char *)mmap(NULL, span, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd, base);
+            CK(hipHostRegister(m, span, hipHostRegisterMapped));
+            void *dm = nullptr;
+            CK(hipHostGetDevicePointer(&dm, m, 0));
+            for (int r = 0; r < reps; r++) {
+                double a = now_us();
+                hipLaunchKernelGGL(k_swap4, dim3(grid), dim3(256), 0, s, (const uint4 *)duser, (uint4 *)((char *)dm + off), (long long)nv);
+                CK(hipStreamSynchronize(s));
+                t[r] = now_us() - a;
+            }
+            report("fileput_zc_persistent.kernel", t);
+            for (int r = 0; r < reps; r++) {
+                double a = now_us();
+                hipLaunchKernelGGL(k_swap4, dim3(grid), dim3(256), 0, s, (const uint4 *)((char *)dm + off), (uint4 *)((char *)duser), (long long)nv);
+                CK(hipStreamSynchronize(s));
+                t[r] = now_us() - a;
+            }
+            report("fileget_zc_persistent.kernel", t);
+            // the same with SDMA H2D into HBM, then the kernel storing into the file
+            for (int r = 0; r < reps; r++) {
+                double a = now_us();
+                CK(hipMemcpyAsync(dbuf, user, bytes, hipMemcpyHostToDevice, s));
+                hipLaunchKernelGGL(k_swap4, dim3(grid), dim3(256), 0, s, (const uint4 *)dbuf, (uint4 *)((char *)dm + off), (long long)nv);
+                CK(hipStreamSynchronize(s));
+                t[r] = now_us() - a;
+            }
+            report("fileput_sdma_zcstore_persistent", t);
+            for (int r = 0; r < reps; r++) {
+                double a = now_us();
+                hipLaunchKernelGGL(k_swap4_x4, dim3((unsigned)((nv + 1023) / 1024)), dim3(256), 0, s, (const uint4 *)((char *)dm + off), (uint4 *)dbuf, (long long)nv);
+                CK(hipMemcpyAsync(user2, dbuf, bytes, hipMemcpyDeviceToHost, s));
+                CK(hipStreamSynchronize(s));
+                t[r] = now_us() - a;
+            }
+            report("fileget_zcx4load_sdma_persistent", t);
+            CK(hipHostUnregister(m));
+            munmap(m, span);
+            // get per call: map + register + kernel (file pages -> user) + unregister + unmap
+            CK(hipHostUnregister(user));
+            CK(hipHostRegister(user2, bytes, hipHostRegisterMapped));
+            void *duser2 = nullptr;
+            CK(hipHostGetDevicePointer(&duser2, user2, 0));
+            for (int r = 0; r < reps; r++) {
+                double a = now_us();
+                unsigned char *mm = (unsigned char *)mmap(NULL, span, PROT_READ, MAP_SHARED | MAP_POPULATE, fd, base);
+                if (mm == MAP_FAILED) return 2;
+                if (hipHostRegister(mm, span, hipHostRegisterMapped | hipHostRegisterReadOnly) != hipSuccess) {
+                    (void)hipGetLastError();
+                    CK(hipHostRegister(mm, span, hipHostRegisterMapped));
+                }
+                void *dmm = nullptr;
+                CK(hipHostGetDevicePointer(&dmm, mm, 0));
+                hipLaunchKernelGGL(k_swap4, dim3(grid), dim3(256), 0, s, (const uint4 *)((char *)dmm + off), (uint4 *)duser2, (long long)nv);
+                CK(hipStreamSynchronize(s));
+                CK(hipHostUnregister(mm));
+                munmap(mm, span);
+                t[r] = now_us() - a;
+            }
+            report("fileget_zc.total(map+reg+kernel+unreg+unmap)", t);
+            for (size_t i = 0; i < bytes / 4; i++)
+                if (user2[i] != user[i]) { fprintf(stderr, "fileget mismatch at %zu\n", i); return 3; }
+            printf("# fileget_zc verified\n");
+            CK(hipHostUnregister(user2));
+        } else {
+            CK(hipHostUnregister(user));
+        }
+    }
     // the reference's sequences, for the same box
     for (int r = 0; r < reps; r++) {
         double a = now_us();
