@@ -583,37 +583,31 @@ def c1_leg(reps=21, n=1 << 20):
 
 
 def c1_reference_sequence(path, var_offset, reps=21, n=1 << 20):
-    """The reference's C1 sequence restated with the oracle on one host
-    thread (cpu_baseline of the c1 leg): put = swap the user buffer in place,
-    pwrite, swap it back (ncmpio_getput.m4:186-214,269-270); get = pread +
-    in-place swap (ncmpio_getput.m4:422-470 -> ncmpio_unpack_xbuf)."""
+    """The reference's C1 sequence restated on one host thread and timed in
+    C (oracle/ref_sequence.c, the cpu_baseline of the c1 leg; an oracle
+    restatement of the reference loop, not the reference binary): put = swap
+    the user buffer in place, pwrite, swap it back (ncmpio_getput.m4:
+    186-214,269-270); get = pread + in-place swap (ncmpio_getput.m4:415-470
+    -> ncmpio_unpack_xbuf)."""
     from oracle import oracle as O
     lib = O.lib()
-    h = (np.arange(n, dtype=np.uint64) * 2654435761 % (1 << 32)).astype(np.uint32)
-    g = np.empty(n, np.uint32)
-    fd = os.open(path, os.O_RDWR)
-    tp, tg = [], []
-    try:
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            lib.orc_in_swapn(h.ctypes.data_as(ctypes.c_void_p), n, 4)
-            os.pwrite(fd, h.data, var_offset)
-            lib.orc_in_swapn(h.ctypes.data_as(ctypes.c_void_p), n, 4)
-            tp.append(time.perf_counter() - t0)
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            os.preadv(fd, [g.data], var_offset)
-            lib.orc_in_swapn(g.ctypes.data_as(ctypes.c_void_p), n, 4)
-            tg.append(time.perf_counter() - t0)
-    finally:
-        os.close(fd)
-    ok = bool(np.array_equal(g, h))
-    put_ms, get_ms = 1e3 * sorted(tp)[reps // 2], 1e3 * sorted(tg)[reps // 2]
+    lib.orc_c1_sequence.argtypes = [ctypes.c_char_p, ctypes.c_longlong, ctypes.c_longlong, ctypes.c_int,
+                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    lib.orc_c1_sequence.restype = ctypes.c_int
+    pm, gm = ctypes.c_double(0), ctypes.c_double(0)
+    rc = lib.orc_c1_sequence(path.encode(), var_offset, n, reps, ctypes.byref(pm), ctypes.byref(gm))
+    put_ms, get_ms = pm.value, gm.value
     xbytes = 4.0 * n
-    return {"value": round(2 * xbytes / ((put_ms + get_ms) * 1e-3) / GIB, 3), "unit": "GiB/s", "cores": 1,
-            "kind": "port", "put_ms": round(put_ms, 4), "get_ms": round(get_ms, 4), "check_ok": ok,
-            "sample": f"the whole C1 request ({n} NC_INT, 4 MiB) on the same tmpfs file, median of {reps}: "
-                      f"orc_in_swapn + pwrite + orc_in_swapn back / pread + orc_in_swapn, 1 thread"}
+    out = {"unit": "GiB/s", "cores": 1, "kind": "port", "check_ok": rc == 0,
+           "sample": f"the whole C1 request ({n} NC_INT, 4 MiB) on the same tmpfs file, median of {reps}: "
+                     f"oracle restatement of the reference loop timed in C (oracle/ref_sequence.c): "
+                     f"orc_in_swapn + pwrite + orc_in_swapn back / pread + orc_in_swapn, 1 thread"}
+    if rc == 0:
+        out.update({"value": round(2 * xbytes / ((put_ms + get_ms) * 1e-3) / GIB, 3),
+                    "put_ms": round(put_ms, 4), "get_ms": round(get_ms, 4)})
+    else:
+        out["error"] = rc
+    return out
 
 
 def c1_workload(cpu=True):

@@ -105,7 +105,7 @@ static const char *const g_ph_names[PH_N] = {
 /* A/B knobs (pncx_shim.h): the environment once at load, then pncx_knob_set */
 static const char *const g_knob_names[PNCXK_NKNOB] = {
     "TILE_U", "XPOSE_MERGE", "URUN", "TMAP_VEC", "IMAP_ROWS", "FUSE_LANES", "BATCH_FUSE", "TMAP_IMAP",
-    "TOFF16", "TOFF_MAX_ELEMS", "XPOSE_ORDER", "TOFF_RUNS", "HOST_ZC", "IO_INLINE_MB", "FILE_WINDOW"};
+    "TOFF16", "TOFF_MAX_ELEMS", "XPOSE_ORDER", "TOFF_RUNS", "HOST_ZC", "IO_INLINE_MB", "FILE_WINDOW", "IO_POPULATE"};
 static long long g_knob[PNCXK_NKNOB];
 
 long long pncx_knob(int id)
@@ -570,9 +570,15 @@ static void unpin_all(pinned_t *pn)
  *               destination directly (zero-copy stores)      the first, 178 all
  *   STAGE_ZC    the kernel loads from and stores to host     2 chunks 149 us
  *               memory (no SDMA)
+ *   STAGE_ALT   as STAGE_COPY, each chunk wholly on one of two streams,
+ *               alternating (round 3's staging)
  * The zero-copy modes need a host destination (and for STAGE_ZC a source)
- * that is pinned or registered; otherwise the chunk is copied. */
-enum { STAGE_COPY = 0, STAGE_ZCOUT = 1, STAGE_ZC = 2 };
+ * that is pinned or registered; otherwise the chunk takes the next mode
+ * down.  STAGE_ZC is the default: 2 GiB in-place 8-byte swap 29-31 GiB/s
+ * of slab against 26-27 for the others; NC_INT -> double 61 GiB/s moved
+ * against 45 for STAGE_COPY; 1 GiB file gets 28-32 GiB/s against 21-25
+ * (profiles/r04j_host_modes.txt). */
+enum { STAGE_COPY = 0, STAGE_ZCOUT = 1, STAGE_ZC = 2, STAGE_ALT = 3 };
 
 struct pncx_stage {
     ctx_t *c;
@@ -641,8 +647,8 @@ static int stage_open(pncx_stage **hp, const op_t *op, int preserve, long long m
     h->din_bytes = ALIGN16((size_t)h->chunk * (size_t)op->ss);
     {
         const long long m = pncx_knob(PNCXK_KNOB_HOST_ZC);
-        h->mode = m < 0 ? STAGE_ZCOUT : (int)m;
-        if (h->mode > STAGE_ZC) h->mode = STAGE_COPY;
+        h->mode = m < 0 ? STAGE_ZC : (int)m;
+        if (h->mode > STAGE_ALT) h->mode = STAGE_COPY;
     }
     pthread_mutex_lock(&c->lock);
     err = stage_slots(c, h->din_bytes + ALIGN16((size_t)h->chunk * (size_t)op->ds));
@@ -736,6 +742,25 @@ int pncx_stage_push(pncx_stage *h, const void *src, void *dst, long long n)
         }
     }
     if (op->ss == op->ds && src == dst) dout = din;            /* in-place swap */
+    if (h->mode == STAGE_ALT) {
+        /* chunk k wholly on stream k & 1; slot k % NDBUF was last used by
+         * chunk k - NDBUF, on the same stream (NDBUF is even) */
+        void *q = c->stream[k & 1];
+        if (!err && ev) err = pncxrt_event_record(ev[0], q);
+        if (!err) err = pncxrt_memcpy_h2d(din, src, (size_t)n * op->ss, q);
+        if (!err && h->preserve && dout != din) err = pncxrt_memcpy_h2d(dout, dst, (size_t)n * op->ds, q);
+        if (!err && ev) err = pncxrt_event_record(ev[1], q);
+        if (!err && !(op->kind == PNCXK_SWAP && op->a == 1 && dout == din))
+            err = launch_op(op, din, dout, n, h->want_status ? c->dstatus : NULL, q);
+        if (!err && ev) err = pncxrt_event_record(ev[2], q);
+        if (!err) err = pncxrt_memcpy_d2h(dst, dout, (size_t)n * op->ds, q);
+        if (!err && ev) err = pncxrt_event_record(ev[3], q);
+        if (!err) err = pncxrt_event_record(c->sev_out[e], q);
+        PH_ADD(PH_CONV_ENQUEUE, t0);
+        if (err) return h->err = err < 0 ? err : PNCX_EDEVICE;
+        h->pushed++;
+        return k;
+    }
     /* the slot's previous chunk must be back on the host */
     if (k >= NDBUF) err = pncxrt_stream_wait_event(si, c->sev_out[(k - NDBUF) % NSEV]);
     if (!err && ev) err = pncxrt_event_record(ev[0], si);

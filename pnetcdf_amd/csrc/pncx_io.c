@@ -30,6 +30,7 @@
 #include "pncx.h"
 #include "pncx_nc.h"
 #include "pncx_io.h"
+#include "pncx_shim.h"
 
 #define MAX_THREADS 64
 #define INLINE_BYTES (1u << 20)      /* below this a job runs in the caller */
@@ -81,12 +82,22 @@ int pio_read_all(int fd, void *buf, size_t n, long long off)
 
 static long g_page;
 
+/* MAP_POPULATE enters a mapping's pages in one pass instead of one fault
+ * each: 4 MiB on one thread 174 us against 514 (tools/c1_probe.hip), but a
+ * 1 GiB put over 8 mapped tasks ran at 18.7 GiB/s with it and 22.3 without
+ * (profiles/r04j_host_modes.txt), and single writers now use pwrite.  Off
+ * by default; PNCX_IO_POPULATE=1 turns it on (A/B). */
+static int populate(void)
+{
+    return pncx_knob(PNCXK_KNOB_IO_POPULATE) == 1 ? MAP_POPULATE : 0;
+}
+
 /* memcpy into a shared mapping of the file (the range lies inside the file) */
 static int map_write(int fd, const unsigned char *src, size_t n, long long off)
 {
     const long long base = off - off % g_page;
     const size_t span = (size_t)(off - base) + n;
-    unsigned char *m = (unsigned char *)mmap(NULL, span, PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd, (off_t)base);
+    unsigned char *m = (unsigned char *)mmap(NULL, span, PROT_WRITE, MAP_SHARED | populate(), fd, (off_t)base);
     if (m == MAP_FAILED) return pio_write_all(fd, src, n, off);
     memcpy(m + (off - base), src, n);
     munmap(m, span);
@@ -117,7 +128,7 @@ static int span_write(int fd, const pio_run *runs, size_t n, long long lo, long 
     if (fmax - fmin > 4 * bytes) return 1;
     base = fmin - fmin % g_page;
     span = (size_t)(fmax - base);
-    m = (unsigned char *)mmap(NULL, span, PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd, (off_t)base);
+    m = (unsigned char *)mmap(NULL, span, PROT_WRITE, MAP_SHARED | populate(), fd, (off_t)base);
     if (m == MAP_FAILED) return 1;
     for (i = 0, pos = 0; i < n && pos < hi; i++) {
         const long long a = pos, b = pos + runs[i].len;

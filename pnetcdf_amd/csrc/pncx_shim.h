@@ -167,6 +167,7 @@ enum {
                                  * stores (default), 2 zero-copy both ways   */
     PNCXK_KNOB_IO_INLINE_MB,    /* requests below: I/O on the calling thread */
     PNCXK_KNOB_FILE_WINDOW,     /* tmpfs file windows: 0 off, 2 at first use */
+    PNCXK_KNOB_IO_POPULATE,     /* 0: mapped writes fault their pages in     */
     PNCXK_NKNOB
 };
 long long pncx_knob(int id);
