@@ -241,6 +241,9 @@ def cpu_c4_jobs(lib, erange, nel=1 << 20, nvar=256, seed=0):
     return jobs, keep
 
 
+PCIE_GBPS = 57.5     # pinned H2D on the MI355X host, profiles/r01_pcie.json
+
+
 def gather_leg(torch, group, buf, gib, chunk_gib, to_cpu=False):
     """Config 5's exchange, timed apart from the conversion rate (SURVEY
     §8(e)): every rank's first `gib` GiB of converted records are gathered
@@ -268,10 +271,16 @@ def gather_leg(torch, group, buf, gib, chunk_gib, to_cpu=False):
     el = group.max([time.perf_counter() - t0])[0]
     ok = all(int(a.item()) == want for got_k, sums_k in zip(arrived, sums) for a, want in zip(got_k, sums_k))
     into = (group.world - 1) * n * 8                         # rank 0's own slice is local
+    rate = into / el / 1e9
     return {"collective": "gather into rank 0 (RCCL over xGMI)" if not to_cpu else "gather into rank 0 (gloo rehearsal)",
             "bytes_per_rank": n * 8, "bytes_into_rank0": into, "chunk_bytes_per_rank": step * 8,
-            "chunks": len(chunks), "ms": round(el * 1e3, 3), "GBps_into_rank0": round(into / el / 1e9, 2),
-            "checksums_ok": ok, "note": "timed region includes one int64 sum kernel per arrived chunk on rank 0"}
+            "chunks": len(chunks), "ms": round(el * 1e3, 3), "GBps_into_rank0": round(rate, 2),
+            "checksums_ok": ok,
+            # xGMI into one GPU is ~7 x 153 GB/s; a gather that does
+            # not beat the PCIe link (57.5 GB/s H2D, profiles/r01_pcie.json)
+            # went through the host, not xGMI
+            "via_xgmi": (not to_cpu) and rate > PCIE_GBPS, "pcie_ceiling_GBps": PCIE_GBPS,
+            "note": "timed region includes one int64 sum kernel per arrived chunk on rank 0"}
 
 
 def load_traffic(kernel_key, elems_per_launch):
@@ -756,20 +765,29 @@ def worker(args):
     del wl
     torch.cuda.empty_cache()
 
-    # ------------------------------------------------ the other 1-GPU configs
-    if world == 1 and not args.no_extra and head == "c2":
+    # ------------------------------------------------ the other configs
+    # C3 and C4 run at every N: each rank converts its own copy of the
+    # workload (the reference's decomposition: per-rank subarrays with no
+    # communication in the conversion, ncmpio_i_getput.m4:332,416), timed
+    # between barriers with the max over ranks, checks AND-reduced; value =
+    # the bytes of all ranks / that time.  C1 is the one-rank file case.
+    if not args.no_extra and head == "c2":
         extra = {}
         for name in EXTRA:
             w = make_workload(name, torch, lib, sptr, args, world, rank)
             el, km, cm = measure(torch, lib, group, stream, w, args.extra_steps, max(args.warmup, args.extra_warmup))
             v, mps, rf = summary(w, el, km, cm, args.extra_steps, world)
             extra[name] = {"value": round(v, 2), "unit": "GiB/s", "ms_per_step": round(mps, 4),
-                           "steps": args.extra_steps, "dtype": w.dtype, "config": w.cfg, "roofline": rf,
-                           "check_ok": w.check(), "check": w.check_desc}
+                           "steps": args.extra_steps, "n_gpus": world, "scaling": "weak", "dtype": w.dtype,
+                           "config": w.cfg, "roofline": rf, "check_ok": group.all_true(w.check()),
+                           "check": w.check_desc + (" (on every rank, AND-reduced)" if world > 1 else "")}
+            if world > 1:
+                extra[name]["kernel_ms_per_rank"] = [round(r[0], 4) for r in
+                                                     group.all_gather_floats([w.rank_kernel_ms])]
             w.free()
             del w
             torch.cuda.empty_cache()
-        if not args.no_c1:
+        if world == 1 and not args.no_c1:
             extra["c1"] = c1_workload(cpu=rank == 0 and not args.no_cpu_baseline)
         line["workloads"] = extra
 

@@ -275,6 +275,20 @@ int pncx_getn_flex(int cdf_ver, int xtype, const void *xbuf, void *buf, int ndim
                    const pncx_offset *count, const pncx_offset *imap, pncx_offset bufcount,
                    const pncx_dtype *buftype);
 
+/* MPI_Pack / MPI_Unpack in HBM: bufcount copies of a committed buftype
+ * between a user buffer and a contiguous packed buffer of its elements, both
+ * on the device, no conversion -- the first step of ncmpio_pack_xbuf
+ * (ncmpio_util.c:620-652) and the last of ncmpio_unpack_xbuf (:889-933),
+ * used where a packed copy is needed (the flexible varn and bput calls on
+ * device buffers).  stream NULL: the call waits for completion. */
+int pncx_dev_pack(void *dpacked, const void *dbuf, pncx_offset bufcount, const pncx_dtype *buftype,
+                  pncx_stream_t stream);
+int pncx_dev_unpack(const void *dpacked, void *dbuf, pncx_offset bufcount, const pncx_dtype *buftype,
+                    pncx_stream_t stream);
+/* Device memory on the current device (hipMalloc), for such packed copies. */
+void *pncx_dev_alloc(pncx_offset nbytes);
+int   pncx_dev_free(void *p);
+
 /* ------------------------------------------------------------------------ */
 /* Data comparison of ncmpidiff (src/utils/ncmpidiff/ncmpidiff_core.c:200-  */
 /* 236, CHECK_VAR_DIFF): the smallest index at which two HBM arrays of      */

@@ -44,6 +44,7 @@ typedef struct stage_t {       /* a flexible varn request staged through a packe
     void *user;
     MPI_Offset bufcount;
     MPI_Datatype buftype;      /* duplicated; freed with the stage */
+    pncx_dtype *dt;            /* device buffers: the committed buftype, tmp in HBM */
 } stage_t;
 
 typedef struct NCM {
@@ -197,8 +198,42 @@ static int unpack_flex(const void *tmp, MPI_Offset want, int itype, void *buf, M
     return NC_NOERR;
 }
 
+/* a packed copy in HBM for a derived buftype over a device buffer: the
+ * MPI library here is not GPU-aware, so the pack is pncx_dev_pack (the
+ * typemap kernels) instead of MPI_Pack */
+static int pack_flex_dev(const void *buf, MPI_Offset bufcount, MPI_Datatype buftype, MPI_Offset want, int pack,
+                         void **tmp, int *itype, pncx_dtype **dt)
+{
+    pncx_offset tn = 0;
+    int err;
+    *tmp = NULL;
+    *dt = NULL;
+    if ((err = pncx_mpi_type_commit(buftype, dt)) != NC_NOERR) return err;
+    pncx_type_inq(*dt, itype, &tn, NULL, NULL);
+    if (bufcount < 0 || tn * bufcount != want) err = NC_EIOMISMATCH;
+    if (!err && (*tmp = pncx_dev_alloc(want * pncx_ilen(*itype) + 16)) == NULL) err = PNCX_EDEVICE;
+    if (!err && pack) err = pncx_dev_pack(*tmp, buf, bufcount, *dt, NULL);
+    if (err) {
+        pncx_dev_free(*tmp);
+        pncx_type_free(*dt);
+        *tmp = NULL;
+        *dt = NULL;
+    }
+    return err;
+}
+
+static void free_packed(void *tmp, pncx_dtype *dt)
+{
+    if (dt != NULL) {
+        pncx_dev_free(tmp);
+        pncx_type_free(dt);
+    } else {
+        free(tmp);
+    }
+}
+
 static int add_stage(NCM *m, int reqid, int get, void *tmp, void *user, MPI_Offset bufcount,
-                     MPI_Datatype buftype)
+                     MPI_Datatype buftype, pncx_dtype *dt)
 {
     stage_t *s;
     if (m->nstage == m->capstage) {
@@ -214,6 +249,7 @@ static int add_stage(NCM *m, int reqid, int get, void *tmp, void *user, MPI_Offs
     s->tmp = tmp;
     s->user = user;
     s->bufcount = bufcount;
+    s->dt = dt;
     if (MPI_Type_dup(buftype, &s->buftype) != MPI_SUCCESS) return NC_EMPI;
     m->nstage++;
     return NC_NOERR;
@@ -229,7 +265,10 @@ static int finish_stages(NCM *m, int nreqs, const int *ids, int unpack)
                   (nreqs == NC_GET_REQ_ALL && s->get);
         for (k = 0; k < nreqs && !hit; k++) hit = ids[k] == s->reqid;
         if (!hit) { i++; continue; }
-        if (unpack && s->get) {
+        if (unpack && s->get && s->dt != NULL) {
+            const int e2 = pncx_dev_unpack(s->tmp, s->user, s->bufcount, s->dt, NULL);
+            if (err == NC_NOERR) err = e2;
+        } else if (unpack && s->get) {
             int itype;
             MPI_Offset nblk, ext, *disp = NULL, *blen = NULL, per = 0, j;
             if (pncx_mpi_type_flatten(s->buftype, &itype, &nblk, &disp, &blen, &ext) == NC_NOERR) {
@@ -240,7 +279,7 @@ static int finish_stages(NCM *m, int nreqs, const int *ids, int unpack)
                                                        s->buftype);
             }
         }
-        free(s->tmp);
+        free_packed(s->tmp, s->dt);
         MPI_Type_free(&s->buftype);
         m->stages[i] = m->stages[--m->nstage];
     }
@@ -737,19 +776,25 @@ static int drv_get_var(void *ncp, int varid, const MPI_Offset *start, const MPI_
 /* a varn buffer as (contiguous pointer, itype): predefined types directly,
  * derived buftypes through a packed copy */
 static int varn_buffer(NCM *m, int varid, int num, MPI_Offset *const *counts, const void *buf,
-                       MPI_Offset bufcount, MPI_Datatype buftype, int pack, void **tmp, const void **ptr, int *itype)
+                       MPI_Offset bufcount, MPI_Datatype buftype, int pack, void **tmp, const void **ptr, int *itype,
+                       pncx_dtype **dt)
 {
     MPI_Offset want = varn_nelems(m, varid, num, counts);
     *tmp = NULL;
     *ptr = buf;
+    *dt = NULL;
     if (direct_itype(m, varid, bufcount, buftype, itype)) {
         if (*itype == 0) return NC_EBADTYPE;
         if (bufcount != -1 && buftype != MPI_DATATYPE_NULL && bufcount != want) return NC_EIOMISMATCH;
         return NC_NOERR;
     }
-    /* a derived buftype over a buffer in HBM would need a device-side
-     * MPI_Pack (the MPI library here is not GPU-aware) */
-    if (pncx_is_device_ptr(buf)) return NC_ENOTSUPPORT;
+    /* a derived buftype over a buffer in HBM: packed on the device */
+    if (pncx_is_device_ptr(buf)) {
+        int err = pack_flex_dev(buf, bufcount, buftype, want, pack, tmp, itype, dt);
+        if (err) return err;
+        *ptr = *tmp;
+        return NC_NOERR;
+    }
     {
         int err = pack_flex(buf, bufcount, buftype, want, pack, tmp, itype);
         if (err) return err;
@@ -766,11 +811,12 @@ static int drv_put_varn(void *ncp, int varid, int num, MPI_Offset *const *starts
     void *tmp = NULL;
     const void *ptr;
     const MPI_Offset before = my_numrecs(m);
+    pncx_dtype *dt = NULL;
     if (!(reqMode & NC_REQ_ZERO)) {
-        err = varn_buffer(m, varid, num, counts, buf, bufcount, buftype, 1, &tmp, &ptr, &it);
+        err = varn_buffer(m, varid, num, counts, buf, bufcount, buftype, 1, &tmp, &ptr, &it, &dt);
         if (!err) err = pncx_nc_put_varn(m->ncid, varid, num, (const pncx_offset *const *)starts,
                                          (const pncx_offset *const *)counts, ptr, it);
-        free(tmp);
+        free_packed(tmp, dt);
     }
     e2 = coll_put_done(m, varid, reqMode, before);
     return (err == NC_NOERR || err == NC_ERANGE) && e2 != NC_NOERR ? e2 : err;
@@ -783,15 +829,17 @@ static int drv_get_varn(void *ncp, int varid, int num, MPI_Offset *const *starts
     int err, it;
     void *tmp = NULL;
     const void *ptr;
+    pncx_dtype *dt = NULL;
     if (reqMode & NC_REQ_ZERO) return NC_NOERR;
-    err = varn_buffer(m, varid, num, counts, buf, bufcount, buftype, 0, &tmp, &ptr, &it);
+    err = varn_buffer(m, varid, num, counts, buf, bufcount, buftype, 0, &tmp, &ptr, &it, &dt);
     if (!err) err = pncx_nc_get_varn(m->ncid, varid, num, (const pncx_offset *const *)starts,
                                      (const pncx_offset *const *)counts, (void *)ptr, it);
     if (tmp != NULL && (err == NC_NOERR || err == NC_ERANGE)) {
-        const int e2 = unpack_flex(tmp, varn_nelems(m, varid, num, counts), it, buf, bufcount, buftype);
+        const int e2 = dt != NULL ? pncx_dev_unpack(tmp, buf, bufcount, dt, NULL)
+                                  : unpack_flex(tmp, varn_nelems(m, varid, num, counts), it, buf, bufcount, buftype);
         if (e2) err = e2;
     }
-    free(tmp);
+    free_packed(tmp, dt);
     return err;
 }
 
@@ -840,10 +888,17 @@ static int drv_bput_var(void *ncp, int varid, const MPI_Offset *start, const MPI
         }
         return pncx_nc_bput_varm(m->ncid, varid, start, count, stride, imap, buf, it, reqid);
     }
-    /* derived buftype: packed now, converted into the attached buffer now */
-    if (pncx_is_device_ptr(buf)) return NC_ENOTSUPPORT;     /* see varn_buffer */
+    /* derived buftype: packed now (on the device for a device buffer),
+     * converted into the attached buffer now (ncmpio_i_getput.m4:266-310) */
     pncx_nc_inq_var(m->ncid, varid, NULL, NULL, &ndims, NULL, NULL);
     for (d = 0; d < ndims; d++) want *= count[d];
+    if (pncx_is_device_ptr(buf)) {
+        pncx_dtype *dt = NULL;
+        if ((err = pack_flex_dev(buf, bufcount, buftype, want, 1, &tmp, &it, &dt)) != NC_NOERR) return err;
+        err = pncx_nc_bput_varm(m->ncid, varid, start, count, stride, imap, tmp, it, reqid);
+        free_packed(tmp, dt);
+        return err;
+    }
     if ((err = pack_flex(buf, bufcount, buftype, want, 1, &tmp, &it)) != NC_NOERR) return err;
     err = pncx_nc_bput_varm(m->ncid, varid, start, count, stride, imap, tmp, it, reqid);
     free(tmp);
@@ -857,14 +912,15 @@ static int drv_iget_varn(void *ncp, int varid, int num, MPI_Offset *const *start
     int err, it, id = NC_REQ_NULL;
     void *tmp = NULL;
     const void *ptr;
+    pncx_dtype *dt = NULL;
     (void)reqMode;
-    err = varn_buffer(m, varid, num, counts, buf, bufcount, buftype, 0, &tmp, &ptr, &it);
+    err = varn_buffer(m, varid, num, counts, buf, bufcount, buftype, 0, &tmp, &ptr, &it, &dt);
     if (!err) err = pncx_nc_iget_varn(m->ncid, varid, num, (const pncx_offset *const *)starts,
                                       (const pncx_offset *const *)counts, (void *)ptr, it, &id);
     if (reqid) *reqid = id;
     if (tmp != NULL) {
-        if (err == NC_NOERR && id != NC_REQ_NULL) err = add_stage(m, id, 1, tmp, buf, bufcount, buftype);
-        else free(tmp);
+        if (err == NC_NOERR && id != NC_REQ_NULL) err = add_stage(m, id, 1, tmp, buf, bufcount, buftype, dt);
+        else free_packed(tmp, dt);
     }
     return err;
 }
@@ -876,14 +932,15 @@ static int drv_iput_varn(void *ncp, int varid, int num, MPI_Offset *const *start
     int err, it, id = NC_REQ_NULL;
     void *tmp = NULL;
     const void *ptr;
+    pncx_dtype *dt = NULL;
     (void)reqMode;
-    err = varn_buffer(m, varid, num, counts, buf, bufcount, buftype, 1, &tmp, &ptr, &it);
+    err = varn_buffer(m, varid, num, counts, buf, bufcount, buftype, 1, &tmp, &ptr, &it, &dt);
     if (!err) err = pncx_nc_iput_varn(m->ncid, varid, num, (const pncx_offset *const *)starts,
                                       (const pncx_offset *const *)counts, ptr, it, &id);
     if (reqid) *reqid = id;
     if (tmp != NULL) {
-        if (err == NC_NOERR && id != NC_REQ_NULL) err = add_stage(m, id, 0, tmp, NULL, 0, buftype);
-        else free(tmp);
+        if (err == NC_NOERR && id != NC_REQ_NULL) err = add_stage(m, id, 0, tmp, NULL, 0, buftype, dt);
+        else free_packed(tmp, dt);
     }
     return err;
 }
@@ -895,11 +952,12 @@ static int drv_bput_varn(void *ncp, int varid, int num, MPI_Offset *const *start
     int err, it;
     void *tmp = NULL;
     const void *ptr;
+    pncx_dtype *dt = NULL;
     (void)reqMode;
-    err = varn_buffer(m, varid, num, counts, buf, bufcount, buftype, 1, &tmp, &ptr, &it);
+    err = varn_buffer(m, varid, num, counts, buf, bufcount, buftype, 1, &tmp, &ptr, &it, &dt);
     if (!err) err = pncx_nc_bput_varn(m->ncid, varid, num, (const pncx_offset *const *)starts,
                                       (const pncx_offset *const *)counts, ptr, it, reqid);
-    free(tmp);
+    free_packed(tmp, dt);
     return err;
 }
 

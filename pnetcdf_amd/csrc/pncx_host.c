@@ -1211,6 +1211,8 @@ struct pncx_dtype {
     long long  rn1, rn2, rs1, rs2;    /* table runs on a 2-level lattice: run i at
                                        * disp0 + (i % rn1)*rs1 + (i / rn1)*rs2 bytes
                                        * (rn1 = 0: not one) */
+    struct pncx_dtype *bytes;         /* the same typemap in bytes (pncx_dev_pack), made on first use */
+    pthread_mutex_t bytes_lock;
 };
 
 /* Largest typemap (elements per copy) that gets a per-element offset map:
@@ -1250,6 +1252,7 @@ int pncx_type_commit(int itype, pncx_offset nblocks, const pncx_offset *disp,
     t->isz = isz;
     t->extent = extent;
     t->refs = 1;
+    pthread_mutex_init(&t->bytes_lock, NULL);
     /* normalise: drop empty runs, merge runs that continue each other */
     for (i = 0; i < nblocks; i++) {
         if (blocklen[i] == 0) continue;
@@ -1415,6 +1418,8 @@ int pncx_type_free(pncx_dtype *t)
         pncxrt_free(t->dtab);
         pncxrt_free(t->doff);
     }
+    if (t->bytes) pncx_type_free(t->bytes);
+    pthread_mutex_destroy(&t->bytes_lock);
     free(t->pre);
     free(t->disp);
     free(t);
@@ -1538,6 +1543,72 @@ int pncx_dev_putn_flex(int cdf_ver, int xtype, void *dxbuf, const void *dbuf, in
     if (n <= 0) return NC_NOERR;
     if (!have_device() || (m.tmode >= 2 && m.tpre == NULL)) return PNCX_EDEVICE;
     return launch_imap_op(&op, (const char *)dbuf + koff, dxbuf, n, &m, 1, dstatus, stream);
+}
+
+/* the typemap of t with its runs counted in bytes: MPI_Pack of itype
+ * elements is a byte copy over these runs (no conversion) */
+static const pncx_dtype *type_bytes(pncx_dtype *t)
+{
+    pthread_mutex_lock(&t->bytes_lock);
+    if (t->bytes == NULL && t->itype != PNCX_ITYPE_UCHAR) {
+        long long *bl = (long long *)malloc(sizeof(long long) * (size_t)(t->nblk ? t->nblk : 1)), i;
+        if (bl != NULL) {
+            for (i = 0; i < t->nblk; i++) bl[i] = ((i + 1 < t->nblk ? t->pre[i + 1] : t->tn) - t->pre[i]) * t->isz;
+            if (pncx_type_commit(PNCX_ITYPE_UCHAR, t->nblk, t->disp, bl, t->extent, &t->bytes) != NC_NOERR)
+                t->bytes = NULL;
+            free(bl);
+        }
+    }
+    pthread_mutex_unlock(&t->bytes_lock);
+    return t->itype == PNCX_ITYPE_UCHAR ? t : t->bytes;
+}
+
+/* MPI_Pack / MPI_Unpack in HBM (ncmpio_pack_xbuf's first step,
+ * ncmpio_util.c:620-652; ncmpio_unpack_xbuf's last, :889-933): a byte copy
+ * of the typemap's runs through the typemap kernels (uchar -> NC_UBYTE is a
+ * copy in convert_swap.m4's classification). */
+static int dev_pack_dir(int pack, void *dpacked, void *dbuf, pncx_offset bufcount, const pncx_dtype *bt,
+                        pncx_stream_t stream)
+{
+    const pncx_dtype *tb;
+    pncx_offset cnt;
+    int err;
+    if (bt == NULL || bufcount < 0) return NC_EINVAL;
+    if (bufcount == 0 || bt->tn == 0) return NC_NOERR;
+    if (!have_device()) return PNCX_EDEVICE;
+    if ((tb = type_bytes((pncx_dtype *)bt)) == NULL) return NC_ENOMEM;
+    cnt = bufcount * bt->tn * bt->isz;
+    err = pack ? pncx_dev_putn_flex(PNCX_FORMAT_CDF5, NC_UBYTE, dpacked, dbuf, 1, &cnt, NULL, bufcount, tb, NULL,
+                                    NULL, stream)
+               : pncx_dev_getn_flex(PNCX_FORMAT_CDF5, NC_UBYTE, dpacked, dbuf, 1, &cnt, NULL, bufcount, tb, NULL,
+                                    stream);
+    if (!err && stream == NULL) err = pncxrt_stream_sync(NULL);
+    return err;
+}
+
+int pncx_dev_pack(void *dpacked, const void *dbuf, pncx_offset bufcount, const pncx_dtype *buftype,
+                  pncx_stream_t stream)
+{
+    return dev_pack_dir(1, dpacked, (void *)dbuf, bufcount, buftype, stream);
+}
+
+int pncx_dev_unpack(const void *dpacked, void *dbuf, pncx_offset bufcount, const pncx_dtype *buftype,
+                    pncx_stream_t stream)
+{
+    return dev_pack_dir(0, (void *)dpacked, dbuf, bufcount, buftype, stream);
+}
+
+void *pncx_dev_alloc(pncx_offset nbytes)
+{
+    void *p = NULL;
+    if (nbytes < 0 || !have_device()) return NULL;
+    return pncxrt_malloc(&p, (size_t)nbytes) == 0 ? p : NULL;
+}
+
+int pncx_dev_free(void *p)
+{
+    if (p == NULL) return NC_NOERR;
+    return pncxrt_free(p) == 0 ? NC_NOERR : PNCX_EDEVICE;
 }
 
 int pncx_dev_getn_flex(int cdf_ver, int xtype, const void *dxbuf, void *dbuf, int ndims,

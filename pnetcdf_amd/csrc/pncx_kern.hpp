@@ -1088,6 +1088,7 @@ struct TransposeGeom {
     int64_t tp, tu;          // tiles along P and U
     int64_t ntiles;          // tp * tu * outer
     int     nod;             // outer dims
+    int     diag;            // diagonal tile order: tile (tp, tu) runs as ((tp + tu) % tp_count, tu)
     int64_t ocount[PNCX_MAX_DIMS], ostride_p[PNCX_MAX_DIMS], ostride_u[PNCX_MAX_DIMS];
 };
 
@@ -1282,6 +1283,15 @@ __global__ __launch_bounds__(256, 2) void k_imap_tile(const uint8_t *src, uint8_
                 ubase += i * g.ostride_u[d];
             }
         }
+        // Diagonal order: neighbouring blocks (consecutive b, the ones an XCD
+        // runs at the same time) take tiles of consecutive u; row-major they
+        // share p0, so with a power-of-two leading dimension their packed-side
+        // columns all sit at the same address bits below the 2^k stride.
+        // Shifting p by u spreads them (a bijection on (tp, tu) for fixed tu).
+        if (g.diag) {
+            tp += tu;
+            if (tp >= g.tp) tp %= g.tp;
+        }
         const int64_t p0 = tp * XT_P, u0 = tu * XT_U;
         const int np = (int)(g.cp - p0 < XT_P ? g.cp - p0 : XT_P), nu = (int)(g.cu - u0 < XT_U ? g.cu - u0 : XT_U);
         if (ALIGNED) {
@@ -1320,6 +1330,7 @@ __global__ __launch_bounds__(256, 2) void k_imap_tile(const uint8_t *src, uint8_
 }
 
 int xpose_merge();   // PNCX_XPOSE_MERGE=0 tiles P alone (A/B); default 1
+int xpose_order();   // PNCX_XPOSE_ORDER: 0 row-major tiles, 1 diagonal, -1 (unset) by shape
 
 // Pick the transpose kernel for a varm layout: P = last dim, U = the other
 // dim with the smallest imap; worth it when P is strided in the user buffer
@@ -1365,6 +1376,15 @@ inline bool transpose_geom(const pncxk_imap *m, TransposeGeom *g, bool merge) {
         outer *= m->count[d];
     }
     g->ntiles = g->tp * g->tu * outer;
+    // diagonal order for tilings of P alone: 8192 x 8192 doubles 52 -> 76 %
+    // (put) and 58-61 -> 74-78 % (get), 16384 x 4096 57-59 -> 80 % (put);
+    // merged 3-D shapes stay row-major: diagonal was 1-2 points slower there,
+    // except x 254 (47-49 -> 50 %; profiles/r04k_xpose_order_ab.txt).
+    // PNCX_XPOSE_ORDER=0 / 1 forces row-major / diagonal.
+    {
+        const int o = xpose_order();
+        g->diag = o < 0 ? !mrg : o == 1;
+    }
     return g->ntiles > 0;
 }
 

@@ -294,6 +294,7 @@ int tile_u(int dflt) {
     return v == 1 || v == 2 || v == 4 ? (int)v : dflt;
 }
 int xpose_merge() { return pncx_knob(PNCXK_KNOB_XPOSE_MERGE) != 0; }
+int xpose_order() { const long long v = pncx_knob(PNCXK_KNOB_XPOSE_ORDER); return v < 0 ? -1 : (int)v; }
 int urun_enabled() { return pncx_knob(PNCXK_KNOB_URUN) != 0; }
 int tmap_vec() { return pncx_knob(PNCXK_KNOB_TMAP_VEC) != 0; }
 int imap_rows() { return pncx_knob(PNCXK_KNOB_IMAP_ROWS) != 0; }

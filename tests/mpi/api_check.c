@@ -528,6 +528,76 @@ static int mode_bputshort(const char *path)
     return nerrs != 0;
 }
 
+/* Derived buftypes over hipMalloc'ed (dev = 1) or host (dev = 0) buffers
+ * through the flexible varn and bput calls (ncmpio_i_varn.m4:165-231,
+ * ncmpio_i_getput.m4:266-310): the user buffer is a 10 x 14 int array whose
+ * 8 x 12 interior (one ghost cell around) is an MPI subarray type.
+ *   a NC_INT:    ncmpi_put_varn_all, two boxes of 4 rows
+ *   b NC_SHORT:  ncmpi_bput_vara (values out of short range: NC_ERANGE at post)
+ *   c NC_DOUBLE: ncmpi_iput_varn + wait_all
+ * then ncmpi_get_varn_all of a and ncmpi_iget_varn of c into fresh
+ * subarray buffers whose ghost cells must survive.  Values: v[i] =
+ * (i * 7919) % 80000 - 40000 over the interior in row-major order. */
+static int mode_flexdev(const char *path, int dev)
+{
+    enum { Y = 8, X = 12, GY = 10, GX = 14 };
+    int ncid, dims[2], va, vb, vc, req[2] = {-1, -1}, st[2] = {-9, -9}, e_bput, i, y, x, bad = 0;
+    int *h = (int *)calloc(GY * GX, sizeof(int)), *g1 = (int *)malloc(GY * GX * sizeof(int)),
+        *g2 = (int *)malloc(GY * GX * sizeof(int));
+    void *buf, *d1 = NULL, *d2 = NULL;
+    MPI_Datatype sub;
+    int sizes[2] = {GY, GX}, subs[2] = {Y, X}, starts[2] = {1, 1};
+    MPI_Offset s0[2] = {0, 0}, s1[2] = {4, 0}, c4[2] = {4, X}, c8[2] = {Y, X};
+    MPI_Offset *vs[2] = {s0, s1}, *vc4[2] = {c4, c4};
+    for (i = 0; i < GY * GX; i++) h[i] = -1;
+    for (y = 0; y < Y; y++)
+        for (x = 0; x < X; x++) h[(y + 1) * GX + x + 1] = (int)(((long long)(y * X + x) * 7919) % 80000) - 40000;
+    MPI_Type_create_subarray(2, sizes, subs, starts, MPI_ORDER_C, MPI_INT, &sub);
+    MPI_Type_commit(&sub);
+    buf = dev ? to_dev(h, GY * GX * sizeof(int)) : (void *)h;
+    CHECK(ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid));
+    CHECK(ncmpi_def_dim(ncid, "y", Y, &dims[0]));
+    CHECK(ncmpi_def_dim(ncid, "x", X, &dims[1]));
+    CHECK(ncmpi_def_var(ncid, "a", NC_INT, 2, dims, &va));
+    CHECK(ncmpi_def_var(ncid, "b", NC_SHORT, 2, dims, &vb));
+    CHECK(ncmpi_def_var(ncid, "c", NC_DOUBLE, 2, dims, &vc));
+    CHECK(ncmpi_enddef(ncid));
+    CHECK(ncmpi_buffer_attach(ncid, Y * X * 8));
+    CHECK(ncmpi_put_varn_all(ncid, va, 2, vs, vc4, buf, 1, sub));
+    e_bput = ncmpi_bput_vara(ncid, vb, s0, c8, buf, 1, sub, &req[0]);
+    CHECK(ncmpi_iput_varn(ncid, vc, 2, vs, vc4, buf, 1, sub, &req[1]));
+    CHECK(ncmpi_wait_all(ncid, 2, req, st));
+    CHECK(ncmpi_buffer_detach(ncid));
+    /* reads back into subarray buffers whose ghosts hold -5 / -6 */
+    for (i = 0; i < GY * GX; i++) { g1[i] = -5; g2[i] = -6; }
+    if (dev) { d1 = to_dev(g1, GY * GX * sizeof(int)); d2 = to_dev(g2, GY * GX * sizeof(int)); }
+    CHECK(ncmpi_get_varn_all(ncid, va, 2, vs, vc4, dev ? d1 : (void *)g1, 1, sub));
+    CHECK(ncmpi_iget_varn(ncid, vc, 2, vs, vc4, dev ? d2 : (void *)g2, 1, sub, &req[0]));
+    CHECK(ncmpi_wait_all(ncid, 1, req, NULL));
+    CHECK(ncmpi_close(ncid));
+    if (dev) {
+        from_dev(g1, d1, GY * GX * sizeof(int));
+        from_dev(g2, d2, GY * GX * sizeof(int));
+        hipFree(d1);
+        hipFree(d2);
+        hipFree(buf);
+    }
+    for (y = 0; y < GY && !bad; y++)
+        for (x = 0; x < GX && !bad; x++) {
+            const int in = y >= 1 && y <= Y && x >= 1 && x <= X, k = y * GX + x;
+            if (g1[k] != (in ? h[k] : -5) || g2[k] != (in ? h[k] : -6)) {
+                fprintf(stderr, "flexdev: get mismatch at (%d, %d): %d %d\n", y, x, g1[k], g2[k]);
+                bad = 1;
+            }
+        }
+    nerrs += bad;
+    MPI_Type_free(&sub);
+    printf("{\"mode\": \"flexdev\", \"dev\": %d, \"bput\": %d, \"wait_status\": [%d, %d], \"errors\": %d}\n",
+           dev, e_bput, st[0], st[1], nerrs);
+    free(h); free(g1); free(g2);
+    return nerrs != 0;
+}
+
 /* errors the dispatcher returns before any conversion (var_getput.m4
  * sanity_check / check_start_count_stride, file.c, attr_getput.m4) */
 static int mode_errors(const char *dir)
@@ -657,6 +727,7 @@ int main(int argc, char **argv)
     else if (argc >= 5 && strcmp(argv[1], "records") == 0) rc = mode_records(argv[2], atoll(argv[3]), atoll(argv[4]));
     else if (argc >= 3 && strcmp(argv[1], "errors") == 0) rc = mode_errors(argv[2]);
     else if (argc >= 3 && strcmp(argv[1], "header") == 0) rc = mode_header(argv[2]);
+    else if (argc >= 4 && strcmp(argv[1], "flexdev") == 0) rc = mode_flexdev(argv[2], atoi(argv[3]));
     else fprintf(stderr, "usage: see the header of api_check.c\n");
     MPI_Finalize();
     return rc;

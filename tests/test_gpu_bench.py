@@ -76,11 +76,19 @@ def test_bench_two_ranks_gloo_twin(gpu):
     checksums, and the rank report (shared device flagged)."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--slab-gib", "0.25",
                         "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--gather-gib", "0.25",
-                        "--gather-chunk-gib", "0.125"],
+                        "--gather-chunk-gib", "0.125", "--extra-steps", "3", "--extra-warmup", "1"],
                        capture_output=True, text=True, timeout=300, env=_env(PNCX_DIST_BACKEND="gloo"), cwd=ROOT)
     line = _line(r)
     assert line["n_gpus"] == 2 and line["check_ok"] is True
     assert line["gather"]["checksums_ok"] is True and line["gather"]["chunks"] == 2
+    # a gloo gather goes through the host: never reported as xGMI
+    assert line["gather"]["via_xgmi"] is False
+    # C3 and C4 per rank at N > 1, checks AND-reduced, kernel time per rank
+    for name in ("c3", "c4", "c4_async", "c4_erange"):
+        w = line["workloads"][name]
+        assert w["check_ok"] is True and w["n_gpus"] == 2, name
+        assert len(w["kernel_ms_per_rank"]) == 2 and w["value"] > 0, name
+    assert "c1" not in line["workloads"]
     rk = line["ranks"]
     assert rk["world_size"] == 2 and rk["backend"] == "gloo" and rk["distinct_devices"] is False
     assert len(rk["kernel_ms_per_rank"]) == 2 and all(k > 0 for k in rk["kernel_ms_per_rank"])

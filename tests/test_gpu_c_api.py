@@ -304,3 +304,26 @@ def test_bput_short_bufcount(gpu, tmp_path):
     the request is NC_EIOMISMATCH, not a read past the buffer."""
     out = _json(capi.run([capi.exe("api_check"), "bputshort", str(tmp_path / "b.nc")]))
     assert out["errors"] == 0 and out["short"] == T.NC_EIOMISMATCH and out["exact"] == 0 and out["status"] == 0
+
+
+@pytest.mark.parametrize("dev", [0, 1], ids=["host", "device"])
+def test_flexible_varn_bput_subarray(gpu, tmp_path, dev):
+    """ncmpi_put_varn_all / ncmpi_bput_vara / ncmpi_iput_varn with an MPI
+    subarray buftype (the interior of a ghosted 10 x 14 int array), from
+    host and hipMalloc'ed buffers: file bytes = MPI_Pack order (the interior,
+    row-major) through the oracle's putn; NC_ERANGE from int -> NC_SHORT is
+    returned by bput at post and not again by wait (ncmpio_i_getput.m4:
+    266-310); get_varn / iget_varn into subarray buffers keep the ghosts
+    (checked in api_check)"""
+    nc = str(tmp_path / "fd.nc")
+    out = _json(capi.run([capi.exe("api_check"), "flexdev", nc, str(dev)]))
+    assert out["errors"] == 0
+    assert out["bput"] == T.NC_ERANGE and out["wait_status"] == [0, 0]
+    vals = ((np.arange(96, dtype=np.int64) * 7919) % 80000 - 40000).astype(np.int32)
+    raw = open(nc, "rb").read()
+    h = cdfparse.parse_cdf(raw)
+    ora = OracleConv()
+    for name, xt in (("a", T.NC_INT), ("b", T.NC_SHORT), ("c", T.NC_DOUBLE)):
+        exp, st = ora.putn(5, xt, vals, T.ITYPE_INT, T.fill_bytes(xt))
+        assert st == (T.NC_ERANGE if xt == T.NC_SHORT else 0)
+        assert _var_bytes(raw, h, name) == exp, name

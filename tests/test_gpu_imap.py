@@ -164,12 +164,28 @@ MERGE_CASES = [
 @pytest.mark.parametrize("count,imap", MERGE_CASES)
 @pytest.mark.parametrize("xt,it", [(T.NC_INT, T.ITYPE_DOUBLE), (T.NC_DOUBLE, T.ITYPE_DOUBLE), (T.NC_UINT64, T.ITYPE_SCHAR)])
 @pytest.mark.parametrize("merge", ["1", "0"])
-def test_imap_tile_merged_dims(torch_cuda, count, imap, xt, it, merge, knob):
+@pytest.mark.parametrize("order", [0, 1], ids=["rowmajor", "diagonal"])
+def test_imap_tile_merged_dims(torch_cuda, count, imap, xt, it, merge, order, knob):
     """k_imap_tile with the last two dimensions tiled as one virtual row
-    (default) and tiled P alone (PNCX_XPOSE_MERGE=0): put and get against a
-    numpy gather/scatter + the oracle, on device buffers."""
+    (default) and tiled P alone (PNCX_XPOSE_MERGE=0), tiles in row-major or
+    diagonal order (PNCX_XPOSE_ORDER): put and get against a numpy
+    gather/scatter + the oracle, on device buffers."""
     knob("XPOSE_MERGE", merge)
+    knob("XPOSE_ORDER", order)
     test_imap_put_get(torch_cuda, count, imap, xt, it, "dev")
+
+
+# 2-D transposes (U = P - 1) with tile grids wider than tall, taller than
+# wide and partial tiles on both edges, in both tile orders
+XPOSE2D_CASES = [([300, 70], [1, 300]), ([70, 300], [1, 70]), ([257, 129], [1, 257]), ([128, 64], [1, 128])]
+
+
+@pytest.mark.parametrize("count,imap", XPOSE2D_CASES)
+@pytest.mark.parametrize("order", [0, 1], ids=["rowmajor", "diagonal"])
+def test_imap_tile_2d_orders(torch_cuda, count, imap, order, knob):
+    knob("XPOSE_ORDER", order)
+    for xt, it in ((T.NC_DOUBLE, T.ITYPE_DOUBLE), (T.NC_SHORT, T.ITYPE_FLOAT)):
+        test_imap_put_get(torch_cuda, count, imap, xt, it, "dev")
 
 
 # varm with a contiguous fastest dimension holding whole 16-byte vectors
