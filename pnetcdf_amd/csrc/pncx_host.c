@@ -1207,7 +1207,7 @@ struct pncx_dtype {
                                        * of a copy (short-run tables, tmode 4), or
                                        * (off16) one base per 64-element chunk
                                        * followed by 16-bit offsets from it (tmode 5) */
-    int        off16;
+    int        off16;                 /* map width: 0 = 32-bit, 1 = 16-bit, 2 = 8-bit gap counts */
     long long  rn1, rn2, rs1, rs2;    /* table runs on a 2-level lattice: run i at
                                        * disp0 + (i % rn1)*rs1 + (i / rn1)*rs2 bytes
                                        * (rn1 = 0: not one) */
@@ -1358,7 +1358,34 @@ int pncx_type_commit(int itype, pncx_offset nblocks, const pncx_offset *disp,
                 const long long ln = (i + 1 < k ? t->pre[i + 1] : t->tn) - t->pre[i];
                 for (e = 0; e < ln; e++) o[t->pre[i] + e] = (unsigned)(t->disp[i] - t->lo + e * isz);
             }
-            if (!derr && k16 != 0) {
+            if (!derr && k16 != 0 && k16 != 16) {
+                /* 8-bit map (tmode 6): element e of chunk q sits ((e & 63) +
+                 * g[e]) elements past the chunk's first element, g counting
+                 * the gap elements before it in the chunk -- 1 B per element
+                 * for typemaps whose offsets rise through each chunk by
+                 * whole elements with under 256 gap elements */
+                const long long nq8 = (t->tn + 63) / 64;
+                unsigned *base = (unsigned *)malloc(sizeof(unsigned) * (size_t)nq8 + (size_t)t->tn);
+                int fits = base != NULL;
+                unsigned char *d8 = fits ? (unsigned char *)(base + nq8) : NULL;
+                for (e = 0; e < t->tn && fits; e++) {
+                    const unsigned b0 = o[e & ~63LL];
+                    long long g;
+                    if ((e & 63) == 0) base[e >> 6] = b0;
+                    fits = o[e] >= b0 && (o[e] - b0) % (unsigned)isz == 0;
+                    g = (long long)((o[e] - b0) / (unsigned)isz) - (e & 63);
+                    fits = fits && g >= 0 && g <= 255;
+                    if (fits) d8[e] = (unsigned char)g;
+                }
+                if (fits) {
+                    bytes = sizeof(unsigned) * (size_t)nq8 + (size_t)t->tn;
+                    up = base;
+                    t->off16 = 2;
+                } else {
+                    free(base);
+                }
+            }
+            if (!derr && k16 != 0 && t->off16 == 0) {
                 const long long nq16 = (t->tn + 63) / 64;
                 unsigned *base = (unsigned *)malloc(sizeof(unsigned) * (size_t)nq16 + sizeof(unsigned short) * (size_t)t->tn);
                 int fits = base != NULL;
@@ -1504,9 +1531,10 @@ static int flex_layout(int ndims, const pncx_offset *count, const pncx_offset *i
         return 1;
     }
     m->tmode = t->layout == 2 && t->runmajor && packed_order ? 3
-             : t->layout == 2 && t->doff ? (t->off16 ? 5 : 4) : t->layout;
+             : t->layout == 2 && t->doff ? (t->off16 == 2 ? 6 : t->off16 ? 5 : 4) : t->layout;
     m->toff = t->doff;
-    m->toff16 = t->off16 ? (const unsigned short *)(t->doff + (t->tn + 63) / 64) : NULL;
+    m->toff16 = t->off16 == 1 ? (const unsigned short *)(t->doff + (t->tn + 63) / 64) : NULL;
+    m->toff8 = t->off16 == 2 ? (const unsigned char *)(t->doff + (t->tn + 63) / 64) : NULL;
     m->tlo = t->lo;
     m->tn = t->tn;
     m->textent = t->extent;

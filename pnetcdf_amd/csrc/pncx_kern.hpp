@@ -861,6 +861,8 @@ template <int ES, typename IDX>
 __device__ __forceinline__ int64_t tmap_byte(int64_t j, const pncxk_imap &m) {
     const IDX c = (IDX)j / (IDX)m.tn;
     const IDX r = (IDX)j - c * (IDX)m.tn;
+    if (m.tmode == 6)
+        return (int64_t)c * m.textent + m.tlo + (int64_t)m.toff[r >> 6] + (int64_t)((r & 63) + m.toff8[r]) * ES;
     if (m.tmode == 5) return (int64_t)c * m.textent + m.tlo + (int64_t)m.toff[r >> 6] + m.toff16[r];
     if (m.tmode == 4) return (int64_t)c * m.textent + m.tlo + (int64_t)m.toff[r];
     if (m.tmode == 1) {

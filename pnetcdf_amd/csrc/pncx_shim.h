@@ -91,7 +91,8 @@ typedef struct pncxk_imap {
      *       3: the same table, runs long enough for one wave per run (packed
      *          order only; runs split into pieces of <= PNCX_TMAP_PIECE)
      *       4: the same table, short runs: per-element byte map toff
-     *       5: the same, 16-bit map: element r at tlo + toff[r >> 6] + toff16[r] */
+     *       5: the same, 16-bit map: element r at tlo + toff[r >> 6] + toff16[r]
+     *       6: the same, 8-bit gap map (toff8, below) */
     int       tmode;
     int       tpad;
     long long tn, textent, tlen, tstride, tdisp0, tnblk;
@@ -105,6 +106,10 @@ typedef struct pncxk_imap {
     /* tmode 5: toff holds one base per 64-element chunk, toff16 the offsets
      * from it (2 B per element instead of 4: chunks spanning < 64 KiB) */
     const unsigned short *toff16;
+    /* tmode 6: toff holds the byte offset of each chunk's first element, toff8
+     * the gap elements before element r in its chunk: r at
+     * tlo + toff[r >> 6] + ((r & 63) + toff8[r]) * element size */
+    const unsigned char *toff8;
 } pncxk_imap;
 
 typedef struct pncxk_opinfo {

@@ -173,16 +173,18 @@ def test_flex_table_search_path(torch_cuda, where, knob):
 
 
 @pytest.mark.parametrize("where", ["host", "dev"])
-@pytest.mark.parametrize("map16", ["1", "0"])
+@pytest.mark.parametrize("map16", ["-1", "16", "0"], ids=["auto8", "16", "32"])
 @pytest.mark.parametrize("gap", [5, 3000])
 def test_flex_offset_map_widths(torch_cuda, where, map16, gap, knob):
-    """short-run tables get a 16-bit offset map (a base per 64-element chunk,
-    tmode 5) when every chunk spans under 64 KiB, else the 32-bit map (tmode
-    4); PNCX_TOFF16=0 forces 32 bits.  Gaps of up to 3000 elements make
-    chunks span ~1.5 MiB of doubles (32-bit map by necessity); partial last
-    chunk and several copies included."""
+    """short-run tables get an 8-bit gap map (tmode 6) when offsets rise
+    through every 64-element chunk with under 256 gap elements, else a
+    16-bit offset map (a base per chunk, tmode 5) when every chunk spans
+    under 64 KiB, else the 32-bit map (tmode 4); PNCX_TOFF16=16 starts at 16
+    bits, 0 forces 32.  Gaps of up to 3000 elements make chunks span ~1.5
+    MiB of doubles (32-bit map by necessity); partial last chunk and several
+    copies included; runs in falling order take the wider maps."""
     knob("TOFF16", map16)
-    rng = np.random.default_rng(gap + int(map16))
+    rng = np.random.default_rng(gap + abs(int(map16)))
     nb = 5000
     blen = rng.integers(1, 8, nb)
     gaps = rng.integers(0, gap, nb)
@@ -190,6 +192,9 @@ def test_flex_offset_map_widths(torch_cuda, where, map16, gap, knob):
     dt = run_case(torch_cuda, where, T.NC_FLOAT, T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(),
                   int(disp[-1] + blen[-1] + 5), 3, None, None, 21)
     assert dt.inq()["layout"] == 2
+    # the same runs in falling order: offsets drop inside chunks
+    run_case(torch_cuda, where, T.NC_FLOAT, T.ITYPE_DOUBLE, disp[::-1].tolist(), blen[::-1].tolist(),
+             int(disp[-1] + blen[-1] + 5), 2, None, None, 23)
     # through a transposing imap as well (imap offset -> typemap stage)
     run_case(torch_cuda, where, T.NC_INT, T.ITYPE_INT, [9, 0, 20, 3, 40], [2, 1, 5, 1, 3], 50, 4, [12, 4], [1, 12], 22)
 

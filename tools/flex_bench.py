@@ -115,9 +115,15 @@ def main():
     res.append(("short_runs", dts.inq()["layout"], n4) + timeit(
         lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(x4.data_ptr()), ctypes.c_void_p(u4.data_ptr()),
                                        1, cp4, None, 8, dts.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n4))
-    os.environ["PNCX_TOFF_MAX_ELEMS"] = "0"              # the same typemap without the offset map
+    pncx.knob_set("TOFF16", 16)                          # the same typemap with the 16-bit map (round 3)
+    dts16 = pncx.DType(T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(), span)
+    pncx.knob_set("TOFF16", -1)
+    res.append(("short_runs_map16", dts16.inq()["layout"], n4) + timeit(
+        lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(x4.data_ptr()), ctypes.c_void_p(u4.data_ptr()),
+                                       1, cp4, None, 8, dts16.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n4))
+    pncx.knob_set("TOFF_MAX_ELEMS", 0)                   # the same typemap without the offset map
     dts2 = pncx.DType(T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(), span)
-    del os.environ["PNCX_TOFF_MAX_ELEMS"]
+    pncx.knob_set("TOFF_MAX_ELEMS", -1)
     res.append(("short_runs_search", dts2.inq()["layout"], n4) + timeit(
         lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(x4.data_ptr()), ctypes.c_void_p(u4.data_ptr()),
                                        1, cp4, None, 8, dts2.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n4))
