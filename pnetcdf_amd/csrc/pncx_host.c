@@ -712,8 +712,8 @@ int pncx_stage_push(pncx_stage *h, const void *src, void *dst, long long n)
     if (pncx_ph_on > 1 && c->pev[4 * PH_EVCH - 1] && h->ph_ev < PH_EVCH) ev = &c->pev[4 * h->ph_ev++];
     if (h->mode != STAGE_COPY && !(op->kind == PNCXK_SWAP && op->a == 1)) {
         /* zero-copy: the kernel writes the host destination itself */
-        void *ddst = pncxrt_host_dptr(dst);
-        const void *dsrc = h->mode == STAGE_ZC ? pncxrt_host_dptr(src) : NULL;
+        void *ddst = pncxrt_host_dptr_range(dst, (size_t)n * op->ds);
+        const void *dsrc = h->mode == STAGE_ZC ? pncxrt_host_dptr_range(src, (size_t)n * op->ss) : NULL;
         if (ddst != NULL && h->mode == STAGE_ZC && dsrc != NULL) {
             void *q = c->stream[k & 1];
             if (!err) err = launch_op(op, dsrc, ddst, n, h->want_status ? c->dstatus : NULL, q);
@@ -2310,10 +2310,48 @@ int pncx_dev_batch_kernel_ms(double *total_ms, long long *calls)
     return NC_NOERR;
 }
 
+/* Zero-copy batch: every segment's host buffers are pinned or registered
+ * for the call, and the batch kernels load from and store to them over PCIe
+ * in one pass (a staged batch copies everything up, converts, copies
+ * everything back).  Returns 1 when it ran (*ret set), 0 when some buffer
+ * could not be mapped (nothing was launched; the caller stages). */
+static int batch_zero_copy(const pncx_seg *segs, int nseg, int *status_out, void *stream, int *ret)
+{
+    pncx_seg *zs = (pncx_seg *)calloc((size_t)nseg, sizeof *zs);
+    void **reg = (void **)calloc((size_t)(2 * nseg), sizeof(void *));
+    int i, nreg = 0, ok = zs != NULL && reg != NULL;
+    for (i = 0; i < nseg && ok; i++) {
+        const pncx_seg *s = &segs[i];
+        const int xs = pncx_xlen(s->xtype), is = pncx_ilen(s->itype);
+        int side;
+        zs[i] = *s;
+        if (xs < 0 || is < 0 || s->nelems <= 0) continue;       /* dev_batch reports these */
+        for (side = 0; side < 2 && ok; side++) {
+            void *h = side ? s->ibuf : s->xbuf;
+            const size_t nb = (size_t)s->nelems * (size_t)(side ? is : xs);
+            void *d = pncxrt_host_dptr_range(h, nb);
+            if (d == NULL) {
+                const int r = pncxrt_host_register(h, nb);
+                if (r == 0) reg[nreg++] = h;
+                d = r >= 0 ? pncxrt_host_dptr_range(h, nb) : NULL;
+            }
+            if (d == NULL) ok = 0;
+            else if (side) zs[i].ibuf = d;
+            else zs[i].xbuf = d;
+        }
+    }
+    if (ok) *ret = pncx_dev_batch(zs, nseg, status_out, stream);
+    for (i = 0; i < nreg; i++) pncxrt_host_unregister(reg[i]);
+    free(zs);
+    free(reg);
+    return ok;
+}
+
 int pncx_batch(const pncx_seg *segs, int nseg, int *status_out)
 {
-    /* Stage every segment into one device arena (16B-aligned slots), run the
-     * device batch, copy the outputs back. */
+    /* Zero copy where every buffer can be mapped (PNCX_HOST_ZC >= 2, the
+     * default); else stage every segment into one device arena (16B-aligned
+     * slots), run the device batch, copy the outputs back. */
     ctx_t *c;
     pncx_seg *dsegs = NULL;
     size_t total = 0, off = 0;
@@ -2323,6 +2361,10 @@ int pncx_batch(const pncx_seg *segs, int nseg, int *status_out)
     if (!have_device()) return PNCX_EDEVICE;
     c = get_ctx();
     if (c == NULL) return PNCX_EDEVICE;
+    {
+        const long long zc = pncx_knob(PNCXK_KNOB_HOST_ZC);
+        if ((zc < 0 || zc == 2) && batch_zero_copy(segs, nseg, status_out, c->stream[0], &ret)) return ret;
+    }
     dsegs = (pncx_seg *)calloc((size_t)nseg, sizeof *dsegs);
     if (dsegs == NULL) return NC_ENOMEM;
     for (i = 0; i < nseg; i++) {

@@ -582,6 +582,16 @@ int pncxrt_host_register_map(void *p, size_t n, int readonly) {
     (void)hipGetLastError();
     return PNCX_EDEVICE;
 }
+void *pncxrt_host_dptr_range(const void *p, size_t n) {
+    /* the device address of [p, p + n) when the whole range is pinned or
+     * registered host memory mapped linearly (its first and last bytes
+     * translate n - 1 apart), else NULL: a range that starts inside one
+     * registration and runs past its end must not reach a kernel */
+    char *a = (char *)pncxrt_host_dptr(p);
+    if (a == nullptr || n == 0) return a;
+    char *b = (char *)pncxrt_host_dptr((const char *)p + (n - 1));
+    return b == a + (n - 1) ? a : nullptr;
+}
 void *pncxrt_host_dptr(const void *p) {
     /* the device address of pinned or registered host memory (the kernels
      * read and write it over PCIe), NULL for pageable or device memory */

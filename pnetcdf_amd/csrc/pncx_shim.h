@@ -212,6 +212,8 @@ int  pncxrt_host_register(void *p, size_t n);
 int  pncxrt_host_unregister(void *p);
 /* device address of pinned/registered host memory, NULL otherwise */
 void *pncxrt_host_dptr(const void *p);
+/* the same for a whole range [p, p + n): NULL unless all of it is mapped */
+void *pncxrt_host_dptr_range(const void *p, size_t n);
 /* register a shared file mapping for device access (read-only or not):
  * 0 = registered, PNCX_EDEVICE = refused */
 int  pncxrt_host_register_map(void *p, size_t n, int readonly);

@@ -80,7 +80,14 @@ def lib():
         "pncx_phase_read": (i, [i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ll)]),
     }
     for name, (res, args) in sig.items():
-        f = getattr(L, name)
+        try:
+            f = getattr(L, name)
+        except AttributeError:
+            # an older build loaded through PNCX_LIB_PATH for an A/B run may
+            # lack the round-4 measurement aids; the product build has all
+            if os.environ.get("PNCX_LIB_PATH") and name.startswith(("pncx_knob", "pncx_phase")):
+                continue
+            raise
         f.restype = res
         f.argtypes = args
     _lib = L

@@ -261,3 +261,31 @@ def test_bput_vara_varn_from_dev(torch_cuda, tmp_path):
     a, _ = ora.putn(5, T.NC_SHORT, f[:200], T.ITYPE_FLOAT, T.fill_bytes(T.NC_SHORT))
     b, _ = ora.putn(5, T.NC_SHORT, f[200:], T.ITYPE_FLOAT, T.fill_bytes(T.NC_SHORT))
     assert _var(raw, "t")[:2 * n] == b + a
+
+
+def test_overlapping_host_buffers_in_one_wait(torch_cuda, tmp_path):
+    """Host buffers reach the batch kernels directly when every segment can
+    be pinned or registered whole (zero-copy batch).  Two iput requests over
+    overlapping parts of one buffer in one wait_all: the second starts inside
+    the first's registration and runs past its end, so it cannot be mapped
+    whole; the batch falls back to staging and converts both correctly"""
+    ora = OracleConv()
+    n = 1 << 18
+    buf = (np.arange(n, dtype=np.int64) * 2654435761 % (1 << 31)).astype(np.int32)
+    p = str(tmp_path / "ov.nc")
+    err, ncid = N.create(p, N.NC_64BIT_DATA)
+    m = 3 * n // 4
+    N.def_dim(ncid, "x", m)
+    N.def_var(ncid, "a", T.NC_INT, [0])
+    N.def_var(ncid, "b", T.NC_DOUBLE, [0])
+    assert N.enddef(ncid) == 0
+    va, vb = buf[:m], buf[n // 4:]                     # overlap: [n/4, 3n/4)
+    e1, r1 = iput(ncid, 0, va, T.ITYPE_INT)
+    e2, r2 = iput(ncid, 1, vb, T.ITYPE_INT)
+    err, st = N.wait_all(ncid, [r1, r2])
+    assert (e1, e2, err, st) == (0, 0, 0, [0, 0])
+    assert N.close(ncid) == 0
+    raw = open(p, "rb").read()
+    for name, xt, vals in (("a", T.NC_INT, va), ("b", T.NC_DOUBLE, vb)):
+        exp, est = ora.putn(5, xt, np.ascontiguousarray(vals), T.ITYPE_INT, T.fill_bytes(xt))
+        assert est == 0 and _var(raw, name) == exp, name

@@ -37,6 +37,7 @@ int pncxrt_ptr_device(const void *p) { (void)p; return -1; }
 int pncxrt_host_register(void *p, size_t n) { (void)p; (void)n; return NODEV; }
 int pncxrt_host_unregister(void *p) { (void)p; return 0; }
 void *pncxrt_host_dptr(const void *p) { (void)p; return NULL; }
+void *pncxrt_host_dptr_range(const void *p, size_t n) { (void)p; (void)n; return NULL; }
 int pncxrt_host_register_map(void *p, size_t n, int r) { (void)p; (void)n; (void)r; return NODEV; }
 const char *pncxrt_last_error(void) { return "no device (host-only ASan build)"; }
 int pncxk_swap(int e, const pncxk_args *a) { (void)e; (void)a; return NODEV; }
