@@ -167,3 +167,32 @@ def test_window_first_touch_rule(gpu, shm_dir, knob):
     for name in ("a", "b"):
         v = [x for x in h["vars"] if x["name"] == name][0]
         assert np.array_equal(np.frombuffer(raw[v["begin"]:v["begin"] + 4 * n], ">i4"), buf)
+
+
+def test_window_churn_guard(gpu, shm_dir, knob):
+    """overlapping requests that slide past the end of the file each need a
+    new window; after four windows used fewer than twice each the file stops
+    making them (each costs ~450 us), and the bytes stay right"""
+    from pnetcdf_amd import pncx
+    knob("FILE_WINDOW", -1)
+    n = 1 << 18                                         # 1 MiB of NC_INT per step
+    p = os.path.join(shm_dir, "churn.nc")
+    err, ncid = N.create(p, N.NC_64BIT_DATA)
+    N.def_dim(ncid, "x", 12 * n)
+    N.def_var(ncid, "v", T.NC_INT, [0])
+    assert N.enddef(ncid) == 0
+    rng = np.random.default_rng(9)
+    ref = np.zeros(12 * n, np.int32)
+    pncx.phases(1)
+    for k in range(10):
+        b = rng.integers(-2**31, 2**31 - 1, 2 * n, dtype=np.int64).astype(np.int32)
+        assert N.put_var(ncid, 0, b, [k * n], [2 * n]) == 0
+        ref[k * n:(k + 2) * n] = b
+    made = pncx.phase_sums().get("file.window_map", (0, 0))[1]
+    pncx.phases(0)
+    assert N.close(ncid) == 0
+    assert made <= 4, made
+    raw = open(p, "rb").read()
+    h = cdfparse.parse_cdf(raw)
+    v = h["vars"][0]
+    assert np.array_equal(np.frombuffer(raw[v["begin"]:v["begin"] + 4 * 11 * n], ">i4"), ref[:11 * n])
