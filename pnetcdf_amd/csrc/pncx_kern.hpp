@@ -1090,7 +1090,7 @@ struct TransposeGeom {
     int64_t tp, tu;          // tiles along P and U
     int64_t ntiles;          // tp * tu * outer
     int     nod;             // outer dims
-    int     diag;            // diagonal tile order: tile (tp, tu) runs as ((tp + tu) % tp_count, tu)
+    int     diag;            // skewed tile order: tile (tp, tu) runs as ((tp + diag * tu) % tp_count, tu); 0 row-major
     int64_t ocount[PNCX_MAX_DIMS], ostride_p[PNCX_MAX_DIMS], ostride_u[PNCX_MAX_DIMS];
 };
 
@@ -1291,7 +1291,7 @@ __global__ __launch_bounds__(256, 2) void k_imap_tile(const uint8_t *src, uint8_
         // columns all sit at the same address bits below the 2^k stride.
         // Shifting p by u spreads them (a bijection on (tp, tu) for fixed tu).
         if (g.diag) {
-            tp += tu;
+            tp += tu * g.diag;
             if (tp >= g.tp) tp %= g.tp;
         }
         const int64_t p0 = tp * XT_P, u0 = tu * XT_U;
@@ -1332,7 +1332,7 @@ __global__ __launch_bounds__(256, 2) void k_imap_tile(const uint8_t *src, uint8_
 }
 
 int xpose_merge();   // PNCX_XPOSE_MERGE=0 tiles P alone (A/B); default 1
-int xpose_order();   // PNCX_XPOSE_ORDER: 0 row-major tiles, 1 diagonal, -1 (unset) by shape
+int xpose_order();   // PNCX_XPOSE_ORDER: 0 row-major tiles, 1 diagonal, k >= 2 skew k, -1 (unset) by shape
 
 // Pick the transpose kernel for a varm layout: P = last dim, U = the other
 // dim with the smallest imap; worth it when P is strided in the user buffer
@@ -1385,7 +1385,7 @@ inline bool transpose_geom(const pncxk_imap *m, TransposeGeom *g, bool merge) {
     // PNCX_XPOSE_ORDER=0 / 1 forces row-major / diagonal.
     {
         const int o = xpose_order();
-        g->diag = o < 0 ? !mrg : o == 1;
+        g->diag = o < 0 ? !mrg : o;      // >= 2: skew of o tiles per u tile
     }
     return g->ntiles > 0;
 }
