@@ -105,7 +105,7 @@ static const char *const g_ph_names[PH_N] = {
 /* A/B knobs (pncx_shim.h): the environment once at load, then pncx_knob_set */
 static const char *const g_knob_names[PNCXK_NKNOB] = {
     "TILE_U", "XPOSE_MERGE", "URUN", "TMAP_VEC", "IMAP_ROWS", "FUSE_LANES", "BATCH_FUSE", "TMAP_IMAP",
-    "TOFF16", "TOFF_MAX_ELEMS", "XPOSE_ORDER", "TOFF_RUNS", "HOST_ZC", "IO_INLINE_MB", "FILE_WINDOW", "IO_POPULATE"};
+    "TOFF16", "TOFF_MAX_ELEMS", "XPOSE_ORDER", "TOFF_RUNS", "HOST_ZC", "IO_INLINE_MB", "FILE_WINDOW", "IO_POPULATE", "HOST_ZC_MAX_MB", "TGAP"};
 static long long g_knob[PNCXK_NKNOB];
 
 long long pncx_knob(int id)
@@ -629,7 +629,19 @@ static long long stage_chunk_elems(const op_t *op, long long n)
     return c < n ? c : (n > 0 ? n : 1);
 }
 
-static int stage_open(pncx_stage **hp, const op_t *op, int preserve, long long max_chunk)
+/* Chunk mode of a call moving `bytes` (input + output): PNCX_HOST_ZC, or by
+ * size -- zero copy up to PNCX_HOST_ZC_MAX_MB (default 64), where a chunk's
+ * fixed costs (a copy command each way) dominate; SDMA copies on alternating
+ * streams above, where the copy engines' bandwidth (57 GB/s each way, both
+ * at once) beats kernels loading host memory (~38 GB/s) */
+static int stage_mode(long long bytes)
+{
+    const long long m = pncx_knob(PNCXK_KNOB_HOST_ZC), mx = pncx_knob(PNCXK_KNOB_HOST_ZC_MAX_MB);
+    if (m >= 0) return m > STAGE_ALT ? STAGE_COPY : (int)m;
+    return bytes <= (mx < 0 ? 64 : mx) * (1LL << 20) ? STAGE_ZC : STAGE_ALT;
+}
+
+static int stage_open(pncx_stage **hp, const op_t *op, int preserve, long long max_chunk, long long total)
 {
     pncx_stage *h;
     ctx_t *c = get_ctx();
@@ -645,11 +657,7 @@ static int stage_open(pncx_stage **hp, const op_t *op, int preserve, long long m
     h->want_status = op->kind != PNCXK_SWAP;
     h->chunk = max_chunk > 0 ? max_chunk : 1;
     h->din_bytes = ALIGN16((size_t)h->chunk * (size_t)op->ss);
-    {
-        const long long m = pncx_knob(PNCXK_KNOB_HOST_ZC);
-        h->mode = m < 0 ? STAGE_ZC : (int)m;
-        if (h->mode > STAGE_ALT) h->mode = STAGE_COPY;
-    }
+    h->mode = stage_mode(total * (long long)(op->ss + op->ds));
     pthread_mutex_lock(&c->lock);
     err = stage_slots(c, h->din_bytes + ALIGN16((size_t)h->chunk * (size_t)op->ds));
     if (!err && h->want_status) {
@@ -674,7 +682,7 @@ static int stage_open(pncx_stage **hp, const op_t *op, int preserve, long long m
 }
 
 int pncx_stage_begin(pncx_stage **hp, int dir, int cdf_ver, int xtype, int itype, const void *fillp,
-                     long long max_chunk)
+                     long long max_chunk, long long total)
 {
     op_t op;
     int err;
@@ -689,7 +697,7 @@ int pncx_stage_begin(pncx_stage **hp, int dir, int cdf_ver, int xtype, int itype
         return err;
     }
     if (!have_device()) return PNCX_EDEVICE;
-    return stage_open(hp, &op, dir == PNCX_PUT ? op.c : 0, max_chunk);
+    return stage_open(hp, &op, dir == PNCX_PUT ? op.c : 0, max_chunk, total);
 }
 
 /* enqueue n (<= the handle's chunk) elements src -> dst; returns the chunk
@@ -883,7 +891,7 @@ static int host_staged(const op_t *op, const void *src, void *dst, long long n, 
     long long off, chunk;
     int err;
     chunk = stage_chunk_elems(op, n);
-    if ((err = stage_open(&h, op, preserve, chunk)) != NC_NOERR) return err;
+    if ((err = stage_open(&h, op, preserve, chunk, n)) != NC_NOERR) return err;
     pin_range(&h->pn, src, (size_t)n * op->ss);
     pin_range(&h->pn, dst, (size_t)n * op->ds);
     for (off = 0; off < n; off += chunk) {
@@ -1207,7 +1215,8 @@ struct pncx_dtype {
                                        * of a copy (short-run tables, tmode 4), or
                                        * (off16) one base per 64-element chunk
                                        * followed by 16-bit offsets from it (tmode 5) */
-    int        off16;                 /* map width: 0 = 32-bit, 1 = 16-bit, 2 = 8-bit gap counts */
+    int        off16;                 /* map width: 0 = 32-bit, 1 = 16-bit, 2 = 8-bit gap counts,
+                                       * 3 = 4-bit gap steps */
     long long  rn1, rn2, rs1, rs2;    /* table runs on a 2-level lattice: run i at
                                        * disp0 + (i % rn1)*rs1 + (i / rn1)*rs2 bytes
                                        * (rn1 = 0: not one) */
@@ -1358,7 +1367,36 @@ int pncx_type_commit(int itype, pncx_offset nblocks, const pncx_offset *disp,
                 const long long ln = (i + 1 < k ? t->pre[i + 1] : t->tn) - t->pre[i];
                 for (e = 0; e < ln; e++) o[t->pre[i] + e] = (unsigned)(t->disp[i] - t->lo + e * isz);
             }
-            if (!derr && k16 != 0 && k16 != 16) {
+            if (!derr && (k16 < 0 || k16 == 4)) {
+                /* 4-bit map (tmode 7): a nibble per element, the gap
+                 * elements between it and the element before it in its
+                 * chunk (0 at a chunk's first), 32 B per chunk after the
+                 * chunk bases (padded to 8 bases: the nibbles stay 32-byte
+                 * aligned) -- 0.5 B per element for typemaps whose runs
+                 * rise through each chunk with gaps of at most 15 elements.
+                 * k_tgap sums a chunk's nibbles across the wave */
+                const long long nq4 = (t->tn + 63) / 64, nqp = (nq4 + 7) & ~7LL;
+                unsigned *base = (unsigned *)calloc(1, sizeof(unsigned) * (size_t)nqp + 32 * (size_t)nq4);
+                int fits = base != NULL;
+                unsigned char *d4 = fits ? (unsigned char *)(base + nqp) : NULL;
+                for (e = 0; e < t->tn && fits; e++) {
+                    if ((e & 63) == 0) {
+                        base[e >> 6] = o[e];
+                        continue;
+                    }
+                    fits = o[e] > o[e - 1] && (o[e] - o[e - 1]) % (unsigned)isz == 0 &&
+                           (o[e] - o[e - 1]) / (unsigned)isz <= 16;
+                    if (fits) d4[e >> 1] |= (unsigned char)(((o[e] - o[e - 1]) / (unsigned)isz - 1) << ((e & 1) * 4));
+                }
+                if (fits) {
+                    bytes = sizeof(unsigned) * (size_t)nqp + 32 * (size_t)nq4;
+                    up = base;
+                    t->off16 = 3;
+                } else {
+                    free(base);
+                }
+            }
+            if (!derr && k16 != 0 && k16 != 16 && t->off16 == 0) {
                 /* 8-bit map (tmode 6): element e of chunk q sits ((e & 63) +
                  * g[e]) elements past the chunk's first element, g counting
                  * the gap elements before it in the chunk -- 1 B per element
@@ -1531,10 +1569,12 @@ static int flex_layout(int ndims, const pncx_offset *count, const pncx_offset *i
         return 1;
     }
     m->tmode = t->layout == 2 && t->runmajor && packed_order ? 3
-             : t->layout == 2 && t->doff ? (t->off16 == 2 ? 6 : t->off16 ? 5 : 4) : t->layout;
+             : t->layout == 2 && t->doff ? (t->off16 == 3 ? 7 : t->off16 == 2 ? 6 : t->off16 ? 5 : 4) : t->layout;
     m->toff = t->doff;
     m->toff16 = t->off16 == 1 ? (const unsigned short *)(t->doff + (t->tn + 63) / 64) : NULL;
-    m->toff8 = t->off16 == 2 ? (const unsigned char *)(t->doff + (t->tn + 63) / 64) : NULL;
+    m->toff8 = t->off16 == 2   ? (const unsigned char *)(t->doff + (t->tn + 63) / 64)
+             : t->off16 == 3 ? (const unsigned char *)(t->doff + (((t->tn + 63) / 64 + 7) & ~7LL))
+                             : NULL;
     m->tlo = t->lo;
     m->tn = t->tn;
     m->textent = t->extent;
@@ -2362,8 +2402,12 @@ int pncx_batch(const pncx_seg *segs, int nseg, int *status_out)
     c = get_ctx();
     if (c == NULL) return PNCX_EDEVICE;
     {
-        const long long zc = pncx_knob(PNCXK_KNOB_HOST_ZC);
-        if ((zc < 0 || zc == 2) && batch_zero_copy(segs, nseg, status_out, c->stream[0], &ret)) return ret;
+        long long bytes = 0;
+        for (i = 0; i < nseg; i++) {
+            const int xs = pncx_xlen(segs[i].xtype), is = pncx_ilen(segs[i].itype);
+            if (xs > 0 && is > 0 && segs[i].nelems > 0) bytes += segs[i].nelems * (long long)(xs + is);
+        }
+        if (stage_mode(bytes) == STAGE_ZC && batch_zero_copy(segs, nseg, status_out, c->stream[0], &ret)) return ret;
     }
     dsegs = (pncx_seg *)calloc((size_t)nseg, sizeof *dsegs);
     if (dsegs == NULL) return NC_ENOMEM;

@@ -23,6 +23,9 @@
 #include "pncx_shim.h"
 
 #include <hip/hip_ext.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 
 namespace pncx {
 
@@ -856,11 +859,33 @@ __device__ __forceinline__ int64_t run_search(const long long *pre, int64_t r, i
     return lo;
 }
 
+// tmode 7 (4-bit gap map): the gap elements before element p of a 64-element
+// chunk are the sum of the chunk's nibbles 0..p (32 bytes, nibble s of byte
+// s/2, low first).  Per-element decode for kernels whose lanes do not cover
+// a chunk each; k_tgap scans the nibbles across the wave instead.
+__device__ __forceinline__ uint32_t nib_prefix(const unsigned char *nib, int64_t q, uint32_t p) {
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(nib + q * 32);
+    uint32_t g = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int lo = i * 16;
+        uint64_t x = w[i];
+        if ((int)p < lo) x = 0;
+        else if ((int)p < lo + 15) x &= (1ULL << ((p - lo + 1) * 4)) - 1;
+        x = (x & 0x0F0F0F0F0F0F0F0FULL) + ((x >> 4) & 0x0F0F0F0F0F0F0F0FULL);
+        g += (uint32_t)((x * 0x0101010101010101ULL) >> 56);
+    }
+    return g;
+}
+
 // any element (imap'ed order): uniform runs by division, tables by search
 template <int ES, typename IDX>
 __device__ __forceinline__ int64_t tmap_byte(int64_t j, const pncxk_imap &m) {
     const IDX c = (IDX)j / (IDX)m.tn;
     const IDX r = (IDX)j - c * (IDX)m.tn;
+    if (m.tmode == 7)
+        return (int64_t)c * m.textent + m.tlo + (int64_t)m.toff[r >> 6] +
+               (int64_t)((r & 63) + nib_prefix(m.toff8, (int64_t)(r >> 6), (uint32_t)(r & 63))) * ES;
     if (m.tmode == 6)
         return (int64_t)c * m.textent + m.tlo + (int64_t)m.toff[r >> 6] + (int64_t)((r & 63) + m.toff8[r]) * ES;
     if (m.tmode == 5) return (int64_t)c * m.textent + m.tlo + (int64_t)m.toff[r >> 6] + m.toff16[r];
@@ -915,6 +940,81 @@ __global__ __launch_bounds__(256) void k_imap(const uint8_t *src, uint8_t *dst, 
             // the subarray case 24 % (5852 -> 4465 GB/s)
             if (k < n) {
                 uint8_t *pd = GATHER ? dst + k * Op::DS : dst + uo[i];
+                const DU o = Op::one(sv[i], old[i], fill, bad);
+                if constexpr (GATHER) st_stream<DU>(pd, o);
+                else st_unaligned<DU>(pd, o);
+            }
+        }
+    }
+    publish(sk, sk.status, bad);
+}
+
+// inclusive sum over the wave's 64 lanes: row shifts 1/2/4/8 inside each
+// 16-lane row, then the row ends broadcast into the rows above (gfx9 DPP
+// row_bcast:15 / row_bcast:31)
+__device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);    // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);    // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true);    // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true);    // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+// Short-run tables with a gap map (tmode TM = 6: 8-bit gap counts, 7: 4-bit
+// gap steps) over a contiguous count of whole copies: one wave per 64-element
+// chunk of a copy, lane p = element p of the chunk.  The copy and chunk come
+// from one wave-uniform division per chunk (k_imap divides every element by
+// tn and decodes its imap), the chunk base is one scalar load, and the 4-bit
+// map's gaps are a wave prefix sum of one nibble per lane.  IMAP_U chunks per
+// wave in flight, loads before stores, unpredicated loads (lanes past the
+// copy's end re-read its last element).  The map width is a template
+// argument: with a run-time switch around the DPP scan the compiler dropped
+// the packed index of the scan path (the store of a tmode-7 chunk went to
+// c*tn + a stale register; found with an address-recording build, round 4).
+template <class Op, bool GATHER, int TM>
+__global__ __launch_bounds__(256) void k_tgap(const uint8_t *src, uint8_t *dst, uint32_t nunits, uint32_t nq,
+                                              pncxk_imap m, typename Op::fill_t fill, Sink sk) {
+    using SU = typename Op::SU;
+    using DU = typename Op::DU;
+    constexpr int UES = GATHER ? Op::SS : Op::DS;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, tn = (uint32_t)m.tn;
+    const uint32_t step = gridDim.x * 4 * IMAP_U;
+    bool bad = false;
+    for (uint32_t u0 = xcd_remap(blockIdx.x, gridDim.x) * 4 * IMAP_U; u0 < nunits; u0 += step) {
+        SU sv[IMAP_U];
+        DU old[IMAP_U];
+        int64_t uo[IMAP_U], ko[IMAP_U];
+        bool ok[IMAP_U];
+#pragma unroll
+        for (int i = 0; i < IMAP_U; i++) {
+            uint32_t u = u0 + i * 4 + w;
+            const bool okw = u < nunits;
+            u = __builtin_amdgcn_readfirstlane(okw ? u : nunits - 1);
+            const uint32_t c = u / nq, q = u - c * nq;
+            const uint32_t r = q * 64 + lane;
+            const uint32_t rc = r < tn ? r : tn - 1;
+            ok[i] = okw && r < tn;
+            ko[i] = (int64_t)c * tn + rc;
+            uint32_t g;
+            if constexpr (TM == 6) {
+                g = m.toff8[rc];
+            } else {
+                static_assert(TM == 7, "k_tgap: 8-bit (6) or 4-bit (7) gap maps");
+                const uint32_t b = m.toff8[(int64_t)q * 32 + (lane >> 1)];
+                g = wave_inclusive_sum((b >> ((lane & 1) * 4)) & 15u);
+            }
+            const int64_t ub = (int64_t)c * m.textent + m.tlo + (int64_t)m.toff[q] + (int64_t)((rc & 63) + g) * UES;
+            uo[i] = ub;
+            sv[i] = ld_unaligned<SU>(GATHER ? src + uo[i] : src + ko[i] * Op::SS);
+            old[i] = 0;
+            if constexpr (Op::PRESERVE) old[i] = ld_unaligned<DU>(GATHER ? dst + ko[i] * Op::DS : dst + uo[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < IMAP_U; i++) {
+            if (ok[i]) {
+                uint8_t *pd = GATHER ? dst + ko[i] * Op::DS : dst + uo[i];
                 const DU o = Op::one(sv[i], old[i], fill, bad);
                 if constexpr (GATHER) st_stream<DU>(pd, o);
                 else st_unaligned<DU>(pd, o);
@@ -1332,6 +1432,7 @@ __global__ __launch_bounds__(256, 2) void k_imap_tile(const uint8_t *src, uint8_
 }
 
 int xpose_merge();   // PNCX_XPOSE_MERGE=0 tiles P alone (A/B); default 1
+int tgap_enabled();  // PNCX_TGAP=0: 8-bit gap maps (tmode 6) on k_imap
 int xpose_order();   // PNCX_XPOSE_ORDER: 0 row-major tiles, 1 diagonal, k >= 2 skew k, -1 (unset) by shape
 
 // Pick the transpose kernel for a varm layout: P = last dim, U = the other
@@ -1465,6 +1566,24 @@ int launch_imap(const pncxk_args *a, const pncxk_imap *m, int gather) {
             } else {
                 if (small) hipLaunchKernelGGL((k_imap_rows<Op, false, uint32_t>), dim3(grid), dim3(256), 0, st, src, dst, nvec, *m, fill, sk);
                 else hipLaunchKernelGGL((k_imap_rows<Op, false, uint64_t>), dim3(grid), dim3(256), 0, st, src, dst, nvec, *m, fill, sk);
+            }
+            return sink_finish(sk, st, grid, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
+        }
+    }
+    if ((m->tmode == 6 || m->tmode == 7) && m->ndims == 1 && m->imap[0] == 1 && m->tn > 0 && a->n % m->tn == 0 &&
+        (m->tmode == 7 || tgap_enabled())) {
+        const int64_t nq = (m->tn + 63) / 64, units = a->n / m->tn * nq;
+        if (m->tn < (1LL << 31) && units < (1LL << 31)) {
+            const int64_t blocks = (units + 4 * IMAP_U - 1) / (4 * IMAP_U);
+            const unsigned grid = (unsigned)(blocks < MAX_BLOCKS ? blocks : MAX_BLOCKS);
+            const Sink sk = sink_acquire(a->status, NC_ERANGE, st, grid, want);
+            const uint32_t nu = (uint32_t)units, q = (uint32_t)nq;
+            if (m->tmode == 7) {
+                if (gather) hipLaunchKernelGGL((k_tgap<Op, true, 7>), dim3(grid), dim3(256), 0, st, src, dst, nu, q, *m, fill, sk);
+                else hipLaunchKernelGGL((k_tgap<Op, false, 7>), dim3(grid), dim3(256), 0, st, src, dst, nu, q, *m, fill, sk);
+            } else {
+                if (gather) hipLaunchKernelGGL((k_tgap<Op, true, 6>), dim3(grid), dim3(256), 0, st, src, dst, nu, q, *m, fill, sk);
+                else hipLaunchKernelGGL((k_tgap<Op, false, 6>), dim3(grid), dim3(256), 0, st, src, dst, nu, q, *m, fill, sk);
             }
             return sink_finish(sk, st, grid, hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE);
         }

@@ -298,6 +298,7 @@ int xpose_order() { const long long v = pncx_knob(PNCXK_KNOB_XPOSE_ORDER); retur
 int urun_enabled() { return pncx_knob(PNCXK_KNOB_URUN) != 0; }
 int tmap_vec() { return pncx_knob(PNCXK_KNOB_TMAP_VEC) != 0; }
 int imap_rows() { return pncx_knob(PNCXK_KNOB_IMAP_ROWS) != 0; }
+int tgap_enabled() { return pncx_knob(PNCXK_KNOB_TGAP) != 0; }
 int fuse_lanes() { return pncx_knob(PNCXK_KNOB_FUSE_LANES) == 1024 ? 1024 : 256; }
 }  // namespace pncx
 

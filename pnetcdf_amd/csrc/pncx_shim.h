@@ -92,7 +92,8 @@ typedef struct pncxk_imap {
      *          order only; runs split into pieces of <= PNCX_TMAP_PIECE)
      *       4: the same table, short runs: per-element byte map toff
      *       5: the same, 16-bit map: element r at tlo + toff[r >> 6] + toff16[r]
-     *       6: the same, 8-bit gap map (toff8, below) */
+     *       6: the same, 8-bit gap map (toff8, below)
+     *       7: the same, 4-bit gap-step map (toff8 holds nibbles, below) */
     int       tmode;
     int       tpad;
     long long tn, textent, tlen, tstride, tdisp0, tnblk;
@@ -108,7 +109,11 @@ typedef struct pncxk_imap {
     const unsigned short *toff16;
     /* tmode 6: toff holds the byte offset of each chunk's first element, toff8
      * the gap elements before element r in its chunk: r at
-     * tlo + toff[r >> 6] + ((r & 63) + toff8[r]) * element size */
+     * tlo + toff[r >> 6] + ((r & 63) + toff8[r]) * element size.
+     * tmode 7: toff8 holds 32 bytes per chunk (32-byte aligned), one nibble
+     * per element (s of chunk q at byte 32q + s/2, low nibble first): the
+     * gap elements between element s-1 and s; the gap count before element
+     * s is the sum of nibbles 0..s of its chunk */
     const unsigned char *toff8;
 } pncxk_imap;
 
@@ -169,10 +174,13 @@ enum {
     PNCXK_KNOB_XPOSE_ORDER,     /* transpose tile order (0 row-major)        */
     PNCXK_KNOB_TOFF_RUNS,       /* 0: short-run tables keep the offset map   */
     PNCXK_KNOB_HOST_ZC,         /* host-buffer chunks: 0 copy, 1 zero-copy
-                                 * stores (default), 2 zero-copy both ways   */
+                                 * stores, 2 zero-copy both ways, 3 copies on
+                                 * alternating streams; unset: by size       */
     PNCXK_KNOB_IO_INLINE_MB,    /* requests below: I/O on the calling thread */
     PNCXK_KNOB_FILE_WINDOW,     /* tmpfs file windows: 0 off, 2 at first use */
     PNCXK_KNOB_IO_POPULATE,     /* 0: mapped writes fault their pages in     */
+    PNCXK_KNOB_HOST_ZC_MAX_MB,  /* largest call given zero-copy chunks       */
+    PNCXK_KNOB_TGAP,            /* 0: 8-bit gap maps stay on k_imap          */
     PNCXK_NKNOB
 };
 long long pncx_knob(int id);

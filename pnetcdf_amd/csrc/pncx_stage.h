@@ -3,7 +3,7 @@
  * HBM (internal to libpncx.so: pncx_host.c implements it, the host-buffer
  * entry points and the file layer's put/get pipelines in pncx_nc.c use it).
  *
- *   pncx_stage_begin(&h, PNCX_PUT, cdf, xtype, itype, fill, chunk_elems);
+ *   pncx_stage_begin(&h, PNCX_PUT, cdf, xtype, itype, fill, chunk_elems, total_elems);
  *   k = pncx_stage_push(h, src, dst, n);   enqueue H2D, kernel, D2H of one chunk
  *   pncx_stage_wait(h, k);                  chunk k's bytes are in dst
  *   st = pncx_stage_end(h);                 wait all; first status (NC_ERANGE)
@@ -27,7 +27,7 @@ extern "C" {
 
 typedef struct pncx_stage pncx_stage;
 int pncx_stage_begin(pncx_stage **h, int dir, int cdf_ver, int xtype, int itype, const void *fillp,
-                     long long max_chunk_elems);
+                     long long max_chunk_elems, long long total_elems);
 int pncx_stage_push(pncx_stage *h, const void *src, void *dst, long long nelems);
 int pncx_stage_wait(pncx_stage *h, int k);
 int pncx_stage_end(pncx_stage *h);

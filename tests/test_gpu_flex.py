@@ -173,17 +173,23 @@ def test_flex_table_search_path(torch_cuda, where, knob):
 
 
 @pytest.mark.parametrize("where", ["host", "dev"])
-@pytest.mark.parametrize("map16", ["-1", "16", "0"], ids=["auto8", "16", "32"])
-@pytest.mark.parametrize("gap", [5, 3000])
-def test_flex_offset_map_widths(torch_cuda, where, map16, gap, knob):
-    """short-run tables get an 8-bit gap map (tmode 6) when offsets rise
-    through every 64-element chunk with under 256 gap elements, else a
+@pytest.mark.parametrize("map16", ["-1", "8", "16", "0"], ids=["auto4", "8", "16", "32"])
+@pytest.mark.parametrize("gap", [5, 16, 17, 3000])
+@pytest.mark.parametrize("tgap", ["-1", "0"], ids=["tgap", "imap"])
+def test_flex_offset_map_widths(torch_cuda, where, map16, gap, tgap, knob):
+    """short-run tables get a 4-bit gap-step map (tmode 7) when offsets rise
+    through every 64-element chunk with gaps of at most 15 elements, else an
+    8-bit gap map (tmode 6) with under 256 gap elements per chunk, else a
     16-bit offset map (a base per chunk, tmode 5) when every chunk spans
-    under 64 KiB, else the 32-bit map (tmode 4); PNCX_TOFF16=16 starts at 16
-    bits, 0 forces 32.  Gaps of up to 3000 elements make chunks span ~1.5
-    MiB of doubles (32-bit map by necessity); partial last chunk and several
-    copies included; runs in falling order take the wider maps."""
+    under 64 KiB, else the 32-bit map (tmode 4); PNCX_TOFF16=8 / 16 start at
+    8 / 16 bits, 0 forces 32.  Gaps of 0..15 fit the nibbles exactly, 0..16
+    do not; gaps of up to 3000 elements make chunks span ~1.5 MiB of doubles
+    (32-bit map by necessity); partial last chunk and several copies
+    included; runs in falling order take the wider maps.  PNCX_TGAP=0 moves
+    the 8-bit map from the wave-per-chunk kernel (k_tgap) to k_imap; the
+    4-bit map always takes k_tgap over whole copies."""
     knob("TOFF16", map16)
+    knob("TGAP", tgap)
     rng = np.random.default_rng(gap + abs(int(map16)))
     nb = 5000
     blen = rng.integers(1, 8, nb)
@@ -197,6 +203,24 @@ def test_flex_offset_map_widths(torch_cuda, where, map16, gap, knob):
              int(disp[-1] + blen[-1] + 5), 2, None, None, 23)
     # through a transposing imap as well (imap offset -> typemap stage)
     run_case(torch_cuda, where, T.NC_INT, T.ITYPE_INT, [9, 0, 20, 3, 40], [2, 1, 5, 1, 3], 50, 4, [12, 4], [1, 12], 22)
+
+
+@pytest.mark.parametrize("where", ["host", "dev"])
+@pytest.mark.parametrize("map16", ["-1", "8"], ids=["map4", "map8"])
+def test_flex_gap_map_through_imap(torch_cuda, where, map16, knob):
+    """rising short runs under a transposing imap: the 4-bit map is decoded
+    per element (a masked nibble sum over the chunk's 32 bytes) by k_imap,
+    the 8-bit map by its lookup; 150 runs span several chunks and end in a
+    partial one"""
+    knob("TOFF16", map16)
+    rng = np.random.default_rng(31)
+    nb = 150
+    blen = rng.integers(1, 8, nb)
+    gaps = rng.integers(0, 16, nb)
+    disp = np.concatenate([[3], 3 + np.cumsum(blen + gaps)[:-1]]).astype(np.int64)
+    tn = int(blen.sum())
+    run_case(torch_cuda, where, T.NC_INT, T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(),
+             int(disp[-1] + blen[-1] + 2), 6, [6, tn], [1, 6], 41)
 
 
 @pytest.mark.parametrize("where", ["host", "dev"])

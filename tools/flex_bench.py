@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--big", action="store_true",
                     help="every workload at >= 4 GiB moved per launch (2^28 elements and more)")
+    ap.add_argument("--short-only", action="store_true",
+                    help="only the short-run workloads (map widths, put and get)")
     args = ap.parse_args()
     big = args.big
     import torch
@@ -63,6 +65,10 @@ def main():
         return ms, n * 16 / ms / 1e6
 
     res = []
+    if args.short_only:
+        short_runs(args, big, torch, T, pncx, lib, st, sp, fp, offs, timeit, res)
+        report(res)
+        return
     # halo3d: 256^3 local array, interior 254^3 (--big: 648^3, interior 646^3)
     L, I = (648, 646) if big else (256, 254)
     ub = torch.empty(L ** 3 * 8, dtype=torch.uint8, device="cuda")
@@ -101,33 +107,7 @@ def main():
                                            ctypes.c_void_p(u2.data_ptr()), 1, cp2, None, 1, dtv.handle, fp,
                                            ctypes.c_void_p(st.data_ptr()), sp), n2))
         del u2, x2
-    # short irregular runs (1..7 elements, gaps 0..4): per-element table search
-    rng = np.random.default_rng(5)
-    nb = 1 << (23 if big else 20)
-    blen = rng.integers(1, 8, nb)
-    disp = np.concatenate([[0], np.cumsum(blen + rng.integers(0, 5, nb))[:-1]]).astype(np.int64) * 8
-    span = int(disp[-1]) + int(blen[-1]) * 8
-    u4 = torch.empty(span * 8, dtype=torch.uint8, device="cuda")
-    dts = pncx.DType(T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(), span)
-    n4 = int(blen.sum()) * 8
-    x4 = torch.empty(n4 * 8, dtype=torch.uint8, device="cuda")
-    c4, cp4 = offs([n4])
-    res.append(("short_runs", dts.inq()["layout"], n4) + timeit(
-        lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(x4.data_ptr()), ctypes.c_void_p(u4.data_ptr()),
-                                       1, cp4, None, 8, dts.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n4))
-    pncx.knob_set("TOFF16", 16)                          # the same typemap with the 16-bit map (round 3)
-    dts16 = pncx.DType(T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(), span)
-    pncx.knob_set("TOFF16", -1)
-    res.append(("short_runs_map16", dts16.inq()["layout"], n4) + timeit(
-        lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(x4.data_ptr()), ctypes.c_void_p(u4.data_ptr()),
-                                       1, cp4, None, 8, dts16.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n4))
-    pncx.knob_set("TOFF_MAX_ELEMS", 0)                   # the same typemap without the offset map
-    dts2 = pncx.DType(T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(), span)
-    pncx.knob_set("TOFF_MAX_ELEMS", -1)
-    res.append(("short_runs_search", dts2.inq()["layout"], n4) + timeit(
-        lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(x4.data_ptr()), ctypes.c_void_p(u4.data_ptr()),
-                                       1, cp4, None, 8, dts2.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n4))
-    del u4, x4
+    short_runs(args, big, torch, T, pncx, lib, st, sp, fp, offs, timeit, res)
     # transpose varm
     cnt = [1024, 1024, 256] if big else [512, 512, 128]
     imap = [1, cnt[0], cnt[0] * cnt[1]]
@@ -153,9 +133,54 @@ def main():
                                            ctypes.c_void_p(u5.data_ptr()), 3, cp5, mp5, T.ITYPE_DOUBLE, fp,
                                            ctypes.c_void_p(st.data_ptr()), sp), n5))
         del u5, x5
+    report(res)
+
+
+def report(res):
     for name, layout, n, ms, gbs in res:
         print(json.dumps({"workload": name, "layout": layout, "n": n, "ms": round(ms, 4),
                           "GB_per_s": round(gbs, 1), "frac_of_8TBs": round(gbs / 8000, 4)}))
+
+
+def short_runs(args, big, torch, T, pncx, lib, st, sp, fp, offs, timeit, res):
+    """short irregular runs (1..7 elements, gaps 0..4) of doubles, 8 copies:
+    the default map (4-bit gap steps, k_tgap), the 8- and 16-bit maps, the
+    get direction, and the per-element table search without a map"""
+    rng = np.random.default_rng(5)
+    nb = 1 << (23 if big else 20)
+    blen = rng.integers(1, 8, nb)
+    disp = np.concatenate([[0], np.cumsum(blen + rng.integers(0, 5, nb))[:-1]]).astype(np.int64) * 8
+    span = int(disp[-1]) + int(blen[-1]) * 8
+    u4 = torch.empty(span * 8, dtype=torch.uint8, device="cuda")
+    dts = pncx.DType(T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(), span)
+    n4 = int(blen.sum()) * 8
+    x4 = torch.empty(n4 * 8, dtype=torch.uint8, device="cuda")
+    c4, cp4 = offs([n4])
+    res.append(("short_runs", dts.inq()["layout"], n4) + timeit(
+        lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(x4.data_ptr()), ctypes.c_void_p(u4.data_ptr()),
+                                       1, cp4, None, 8, dts.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n4))
+    pncx.knob_set("TOFF16", 16)                          # the same typemap with the 16-bit map (round 3)
+    dts16 = pncx.DType(T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(), span)
+    pncx.knob_set("TOFF16", -1)
+    pncx.knob_set("TOFF16", 8)                           # the same typemap with the 8-bit map (round 4)
+    dts8 = pncx.DType(T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(), span)
+    pncx.knob_set("TOFF16", -1)
+    res.append(("short_runs_map8", dts8.inq()["layout"], n4) + timeit(
+        lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(x4.data_ptr()), ctypes.c_void_p(u4.data_ptr()),
+                                       1, cp4, None, 8, dts8.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n4))
+    res.append(("short_runs_get", dts.inq()["layout"], n4) + timeit(
+        lambda: lib.pncx_dev_getn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(x4.data_ptr()), ctypes.c_void_p(u4.data_ptr()),
+                                       1, cp4, None, 8, dts.handle, ctypes.c_void_p(st.data_ptr()), sp), n4))
+    res.append(("short_runs_map16", dts16.inq()["layout"], n4) + timeit(
+        lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(x4.data_ptr()), ctypes.c_void_p(u4.data_ptr()),
+                                       1, cp4, None, 8, dts16.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n4))
+    pncx.knob_set("TOFF_MAX_ELEMS", 0)                   # the same typemap without the offset map
+    dts2 = pncx.DType(T.ITYPE_DOUBLE, disp.tolist(), blen.tolist(), span)
+    pncx.knob_set("TOFF_MAX_ELEMS", -1)
+    res.append(("short_runs_search", dts2.inq()["layout"], n4) + timeit(
+        lambda: lib.pncx_dev_putn_flex(5, T.NC_DOUBLE, ctypes.c_void_p(x4.data_ptr()), ctypes.c_void_p(u4.data_ptr()),
+                                       1, cp4, None, 8, dts2.handle, fp, ctypes.c_void_p(st.data_ptr()), sp), n4))
+    del u4, x4
 
 
 if __name__ == "__main__":
