@@ -629,16 +629,18 @@ static long long stage_chunk_elems(const op_t *op, long long n)
     return c < n ? c : (n > 0 ? n : 1);
 }
 
-/* Chunk mode of a call moving `bytes` (input + output): PNCX_HOST_ZC, or by
- * size -- zero copy up to PNCX_HOST_ZC_MAX_MB (default 64), where a chunk's
- * fixed costs (a copy command each way) dominate; SDMA copies on alternating
- * streams above, where the copy engines' bandwidth (57 GB/s each way, both
- * at once) beats kernels loading host memory (~38 GB/s) */
+/* Chunk mode of a call moving `bytes` (input + output): PNCX_HOST_ZC, else
+ * zero copy both ways, up to PNCX_HOST_ZC_MAX_MB when that is set (SDMA
+ * copies on alternating streams above it).  Zero copy won at every size
+ * measured: 2 GiB round trips 29-31 GiB/s against 27 (alternating copies) and
+ * 25 (copy in / copy out streams); file_bench's big get 32.6 against 22.8
+ * GiB/s, C3 22.3 against 16.4, C4 16.3 against 12.0
+ * (profiles/r04q_host_modes.txt) */
 static int stage_mode(long long bytes)
 {
     const long long m = pncx_knob(PNCXK_KNOB_HOST_ZC), mx = pncx_knob(PNCXK_KNOB_HOST_ZC_MAX_MB);
     if (m >= 0) return m > STAGE_ALT ? STAGE_COPY : (int)m;
-    return bytes <= (mx < 0 ? 64 : mx) * (1LL << 20) ? STAGE_ZC : STAGE_ALT;
+    return mx < 0 || bytes <= mx * (1LL << 20) ? STAGE_ZC : STAGE_ALT;
 }
 
 static int stage_open(pncx_stage **hp, const op_t *op, int preserve, long long max_chunk, long long total)
