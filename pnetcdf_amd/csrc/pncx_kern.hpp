@@ -90,6 +90,19 @@ __device__ __forceinline__ T ld_unaligned(const uint8_t *p) {
     __builtin_memcpy(&t, p, sizeof t);
     return t;
 }
+// nontemporal load from any byte address (gfx950 global loads take
+// unaligned addresses; the under-aligned type keeps the compiler honest)
+template <typename T>
+__device__ __forceinline__ T ld_nt_unaligned(const uint8_t *p) {
+    typedef T __attribute__((aligned(1))) T1;
+    return __builtin_nontemporal_load(reinterpret_cast<const T1 *>(p));
+}
+// nontemporal store (nt, not sc1) to any byte address
+template <typename T>
+__device__ __forceinline__ void st_nt_unaligned(uint8_t *p, T t) {
+    typedef T __attribute__((aligned(1))) T1;
+    __builtin_nontemporal_store(t, reinterpret_cast<T1 *>(p));
+}
 template <typename T>
 __device__ __forceinline__ void st_unaligned(uint8_t *p, T t) {
     __builtin_memcpy(p, &t, sizeof t);
@@ -1007,7 +1020,10 @@ __global__ __launch_bounds__(256) void k_tgap(const uint8_t *src, uint8_t *dst, 
             }
             const int64_t ub = (int64_t)c * m.textent + m.tlo + (int64_t)m.toff[q] + (int64_t)((rc & 63) + g) * UES;
             uo[i] = ub;
-            sv[i] = ld_unaligned<SU>(GATHER ? src + uo[i] : src + ko[i] * Op::SS);
+            // put: the user side's runs are read once -- nontemporal loads,
+            // 4437 -> 4679 GB/s on the short-run layout (tools/tgap_bench.hip)
+            if constexpr (GATHER) sv[i] = ld_nt_unaligned<SU>(src + uo[i]);
+            else sv[i] = ld_unaligned<SU>(src + ko[i] * Op::SS);
             old[i] = 0;
             if constexpr (Op::PRESERVE) old[i] = ld_unaligned<DU>(GATHER ? dst + ko[i] * Op::DS : dst + uo[i]);
         }
@@ -1016,8 +1032,11 @@ __global__ __launch_bounds__(256) void k_tgap(const uint8_t *src, uint8_t *dst, 
             if (ok[i]) {
                 uint8_t *pd = GATHER ? dst + ko[i] * Op::DS : dst + uo[i];
                 const DU o = Op::one(sv[i], old[i], fill, bad);
+                // get: nt stores into the gapped user layout, 2240 -> 2622 GB/s on
+                // the short-run layout (tools/tgap_bench.hip; sc1 write-through
+                // is what hurt split lines in k_imap, plain nt does not)
                 if constexpr (GATHER) st_stream<DU>(pd, o);
-                else st_unaligned<DU>(pd, o);
+                else st_nt_unaligned<DU>(pd, o);
             }
         }
     }

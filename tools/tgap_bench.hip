@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <random>
 #include <vector>
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
     v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);
@@ -48,6 +49,208 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t *src, uint8_t *dst
         for (int i = 0; i < U; i++)
             if (ok[i]) __builtin_nontemporal_store(__builtin_bswap64(sv[i]), (uint64_t *)(dst + ko[i] * 8));
     }
+}
+
+// staged: every unit's map loads first, then the scans, then the element
+// loads, then the stores (explicit software pipelining of the U units)
+template <int U, int BS>
+__global__ __launch_bounds__(BS) void k_gather_st(const uint8_t *src, uint8_t *dst, uint32_t nunits, uint32_t nq,
+                                                  uint32_t tn, int64_t textent, const unsigned *toff,
+                                                  const unsigned char *nib) {
+    constexpr int W = BS / 64;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t step = gridDim.x * W * U;
+    for (uint32_t u0 = blockIdx.x * W * U; u0 < nunits; u0 += step) {
+        uint32_t c[U], q[U], rc[U], b[U], tq[U];
+        bool ok[U];
+#pragma unroll
+        for (int i = 0; i < U; i++) {
+            uint32_t u = u0 + i * W + w;
+            const bool okw = u < nunits;
+            u = __builtin_amdgcn_readfirstlane(okw ? u : nunits - 1);
+            c[i] = u / nq;
+            q[i] = u - c[i] * nq;
+            const uint32_t r = q[i] * 64 + lane;
+            rc[i] = r < tn ? r : tn - 1;
+            ok[i] = okw && r < tn;
+            b[i] = nib[(int64_t)q[i] * 32 + (lane >> 1)];
+            tq[i] = toff[q[i]];
+        }
+        uint64_t sv[U];
+#pragma unroll
+        for (int i = 0; i < U; i++) {
+            const uint32_t g = wave_inclusive_sum((b[i] >> ((lane & 1) * 4)) & 15u);
+            const uint8_t *p = src + (int64_t)c[i] * textent + tq[i] + (int64_t)((rc[i] & 63) + g) * 8;
+            sv[i] = __builtin_nontemporal_load((const uint64_t *)p);
+        }
+#pragma unroll
+        for (int i = 0; i < U; i++)
+            if (ok[i])
+                __builtin_nontemporal_store(__builtin_bswap64(sv[i]), (uint64_t *)(dst + ((int64_t)c[i] * tn + rc[i]) * 8));
+    }
+}
+
+template <int U, int BS>
+float run_st(const uint8_t *s, uint8_t *d, uint32_t nunits, uint32_t nq, uint32_t tn, int64_t ext, const unsigned *t,
+             const unsigned char *nb) {
+    const unsigned grid = (nunits + (BS / 64) * U - 1) / ((BS / 64) * U);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipLaunchKernelGGL((k_gather_st<U, BS>), dim3(grid), dim3(BS), 0, 0, s, d, nunits, nq, tn, ext, t, nb);
+    hipEventRecord(a, 0);
+    for (int k = 0; k < 20; k++)
+        hipLaunchKernelGGL((k_gather_st<U, BS>), dim3(grid), dim3(BS), 0, 0, s, d, nunits, nq, tn, ext, t, nb);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    return ms / 20;
+}
+
+// get direction: packed -> user scatter.  MODE 0: plain 8-byte stores at
+// the user positions (k_tgap today); 1: nontemporal stores; 2: the chunk's
+// user span loaded into LDS, the elements merged there, the span written
+// back whole in 16-byte pieces (gap bytes rewritten with the values read)
+template <int U, int MODE>
+__global__ __launch_bounds__(256) void k_scatter(const uint8_t *src, uint8_t *dst, uint32_t nunits, uint32_t nq,
+                                                 uint32_t tn, int64_t textent, const unsigned *toff,
+                                                 const unsigned char *nib) {
+    constexpr int SLOT = 3072;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[MODE == 2 ? 4 * U * SLOT : 16];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t step = gridDim.x * 4 * U;
+    for (uint32_t u0 = blockIdx.x * 4 * U; u0 < nunits; u0 += step) {
+        uint64_t sv[U];
+        uint8_t *up[U];
+        bool ok[U];
+        uint32_t pos[U], last[U];
+#pragma unroll
+        for (int i = 0; i < U; i++) {
+            uint32_t u = u0 + i * 4 + w;
+            const bool okw = u < nunits;
+            u = __builtin_amdgcn_readfirstlane(okw ? u : nunits - 1);
+            const uint32_t c = u / nq, q = u - c * nq, r = q * 64 + lane, rc = r < tn ? r : tn - 1;
+            ok[i] = okw && r < tn;
+            const uint32_t b = nib[(int64_t)q * 32 + (lane >> 1)];
+            const uint32_t g = wave_inclusive_sum((b >> ((lane & 1) * 4)) & 15u);
+            pos[i] = (rc & 63) + g;
+            last[i] = __builtin_amdgcn_readlane(pos[i], 63);
+            up[i] = dst + (int64_t)c * textent + toff[q];
+            sv[i] = __builtin_nontemporal_load((const uint64_t *)(src + ((int64_t)c * tn + rc) * 8));
+            if (!okw) ok[i] = false;
+        }
+        if constexpr (MODE < 2) {
+#pragma unroll
+            for (int i = 0; i < U; i++) {
+                if (!ok[i]) continue;
+                uint64_t *p = (uint64_t *)(up[i] + pos[i] * 8);
+                if constexpr (MODE == 1) __builtin_nontemporal_store(__builtin_bswap64(sv[i]), p);
+                else *p = __builtin_bswap64(sv[i]);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < U; i++) {
+                uint8_t *sl = lds + (w * U + i) * SLOT;
+                const uint32_t bytes = (last[i] + 1) * 8;            // 8-aligned span from the chunk's first element
+                for (uint32_t o = lane * 8; o < bytes; o += 512)
+                    *(uint64_t *)(sl + o) = *(const uint64_t *)(up[i] + o);
+            }
+#pragma unroll
+            for (int i = 0; i < U; i++) {
+                uint8_t *sl = lds + (w * U + i) * SLOT;
+                if (ok[i]) *(uint64_t *)(sl + pos[i] * 8) = __builtin_bswap64(sv[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < U; i++) {
+                const uint8_t *sl = lds + (w * U + i) * SLOT;
+                const uint32_t bytes = (last[i] + 1) * 8;
+                for (uint32_t o = lane * 8; o < bytes; o += 512)
+                    *(uint64_t *)(up[i] + o) = *(const uint64_t *)(sl + o);
+            }
+        }
+    }
+}
+
+template <int U, int MODE>
+float run_sc(const uint8_t *s, uint8_t *d, uint32_t nunits, uint32_t nq, uint32_t tn, int64_t ext, const unsigned *t,
+             const unsigned char *nb) {
+    const unsigned grid = (nunits + 4 * U - 1) / (4 * U);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipLaunchKernelGGL((k_scatter<U, MODE>), dim3(grid), dim3(256), 0, 0, s, d, nunits, nq, tn, ext, t, nb);
+    hipEventRecord(a, 0);
+    for (int k = 0; k < 20; k++)
+        hipLaunchKernelGGL((k_scatter<U, MODE>), dim3(grid), dim3(256), 0, 0, s, d, nunits, nq, tn, ext, t, nb);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    return ms / 20;
+}
+
+// the chunk's span read whole (16-byte pieces, contiguous per instruction)
+// into LDS, then each lane picks its element from LDS
+template <int U>
+__global__ __launch_bounds__(256) void k_gather_lds(const uint8_t *src, uint8_t *dst, uint32_t nunits, uint32_t nq,
+                                                    uint32_t tn, int64_t textent, const unsigned *toff,
+                                                    const unsigned char *nib) {
+    constexpr int SLOT = 3072;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[4 * U * SLOT];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t step = gridDim.x * 4 * U;
+    for (uint32_t u0 = blockIdx.x * 4 * U; u0 < nunits; u0 += step) {
+        int64_t ko[U];
+        bool ok[U];
+        uint32_t pos[U];
+        uint32_t lo16[U];
+#pragma unroll
+        for (int i = 0; i < U; i++) {
+            uint32_t u = u0 + i * 4 + w;
+            const bool okw = u < nunits;
+            u = __builtin_amdgcn_readfirstlane(okw ? u : nunits - 1);
+            const uint32_t c = u / nq, q = u - c * nq, r = q * 64 + lane, rc = r < tn ? r : tn - 1;
+            ok[i] = okw && r < tn;
+            ko[i] = (int64_t)c * tn + rc;
+            const uint32_t b = nib[(int64_t)q * 32 + (lane >> 1)];
+            const uint32_t g = wave_inclusive_sum((b >> ((lane & 1) * 4)) & 15u);
+            const uint32_t last = __builtin_amdgcn_readlane(g + (rc & 63), 63);   // element offset of the last lane
+            const uint8_t *base = src + (int64_t)c * textent + toff[q];
+            const uintptr_t a0 = (uintptr_t)base & ~(uintptr_t)15;
+            lo16[i] = (uint32_t)((uintptr_t)base - a0);
+            const uint32_t bytes = lo16[i] + (last + 1) * 8;
+            uint8_t *sl = lds + (w * U + i) * SLOT;
+            for (uint32_t o = lane * 16; o < bytes; o += 1024)
+                *(u32x4 *)(sl + o) = __builtin_nontemporal_load((const u32x4 *)(a0 + o));
+            pos[i] = (rc & 63) + g;
+        }
+#pragma unroll
+        for (int i = 0; i < U; i++) {
+            const uint8_t *sl = lds + (w * U + i) * SLOT;
+            uint64_t v;
+            __builtin_memcpy(&v, sl + lo16[i] + pos[i] * 8, 8);
+            if (ok[i]) __builtin_nontemporal_store(__builtin_bswap64(v), (uint64_t *)(dst + ko[i] * 8));
+        }
+    }
+}
+
+template <int U>
+float run_lds(const uint8_t *s, uint8_t *d, uint32_t nunits, uint32_t nq, uint32_t tn, int64_t ext, const unsigned *t,
+              const unsigned char *nb) {
+    const unsigned grid = (nunits + 4 * U - 1) / (4 * U);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipLaunchKernelGGL((k_gather_lds<U>), dim3(grid), dim3(256), 0, 0, s, d, nunits, nq, tn, ext, t, nb);
+    hipEventRecord(a, 0);
+    for (int k = 0; k < 20; k++)
+        hipLaunchKernelGGL((k_gather_lds<U>), dim3(grid), dim3(256), 0, 0, s, d, nunits, nq, tn, ext, t, nb);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    return ms / 20;
 }
 
 template <int U, bool NTL>
@@ -94,13 +297,58 @@ int main() {
     hipMemcpy(t, base.data(), 4 * (size_t)nq, hipMemcpyHostToDevice);
     hipMemcpy(nbp, nib.data(), nib.size(), hipMemcpyHostToDevice);
     const double alg = (double)tn * copies * 16;
-    for (int rep = 0; rep < 2; rep++) {
-        printf("U2 %.1f  U4 %.1f  U8 %.1f  U4nt %.1f  U8nt %.1f GB/s\n",
-               alg / run<2, false>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
+    // correctness of the LDS variant against the plain one
+    {
+        std::vector<uint8_t> hs((size_t)ext * copies);
+        for (size_t i = 0; i < hs.size(); i++) hs[i] = (uint8_t)(i * 2654435761u >> 13);
+        hipMemcpy(s, hs.data(), hs.size(), hipMemcpyHostToDevice);
+        uint8_t *d2;
+        if (hipMalloc(&d2, (size_t)tn * copies * 8)) return 4;
+        run<4, false>(s, d, nunits, nq, tn, ext, t, nbp);
+        run_st<4, 256>(s, d2, nunits, nq, tn, ext, t, nbp);
+        std::vector<uint8_t> h1((size_t)tn * copies * 8), h2(h1.size());
+        hipMemcpy(h1.data(), d, h1.size(), hipMemcpyDeviceToHost);
+        hipMemcpy(h2.data(), d2, h2.size(), hipMemcpyDeviceToHost);
+        printf("staged variant %s the plain gather\n", h1 == h2 ? "matches" : "DIFFERS from");
+        hipFree(d2);
+    }
+    {
+        // scatter modes agree: the user buffer after MODE 0 and MODE 2 from
+        // the same packed input and the same starting user bytes
+        uint8_t *pk, *u1, *u2;
+        const size_t ub = (size_t)ext * copies, pb = (size_t)tn * copies * 8;
+        if (hipMalloc(&pk, pb) || hipMalloc(&u1, ub) || hipMalloc(&u2, ub)) return 4;
+        std::vector<uint8_t> hp(pb), hu(ub);
+        for (size_t i = 0; i < pb; i++) hp[i] = (uint8_t)(i * 2246822519u >> 11);
+        for (size_t i = 0; i < ub; i++) hu[i] = (uint8_t)(i * 3266489917u >> 17);
+        hipMemcpy(pk, hp.data(), pb, hipMemcpyHostToDevice);
+        hipMemcpy(u1, hu.data(), ub, hipMemcpyHostToDevice);
+        hipMemcpy(u2, hu.data(), ub, hipMemcpyHostToDevice);
+        run_sc<4, 0>(pk, u1, nunits, nq, tn, ext, t, nbp);
+        run_sc<2, 2>(pk, u2, nunits, nq, tn, ext, t, nbp);
+        std::vector<uint8_t> h1(ub), h2(ub);
+        hipMemcpy(h1.data(), u1, ub, hipMemcpyDeviceToHost);
+        hipMemcpy(h2.data(), u2, ub, hipMemcpyDeviceToHost);
+        printf("lds-merge scatter %s the plain scatter\n", h1 == h2 ? "matches" : "DIFFERS from");
+        for (int rep = 0; rep < 2; rep++)
+            printf("get: plain4 %.1f  nt4 %.1f  plain2 %.1f  lds1 %.1f  lds2 %.1f GB/s\n",
+                   alg / run_sc<4, 0>(pk, u1, nunits, nq, tn, ext, t, nbp) / 1e6,
+                   alg / run_sc<4, 1>(pk, u1, nunits, nq, tn, ext, t, nbp) / 1e6,
+                   alg / run_sc<2, 0>(pk, u1, nunits, nq, tn, ext, t, nbp) / 1e6,
+                   alg / run_sc<1, 2>(pk, u1, nunits, nq, tn, ext, t, nbp) / 1e6,
+                   alg / run_sc<2, 2>(pk, u1, nunits, nq, tn, ext, t, nbp) / 1e6);
+        hipFree(pk); hipFree(u1); hipFree(u2);
+    }
+    for (int rep = 0; rep < 1; rep++) {
+        printf("U4 %.1f  U4nt %.1f  st4x256 %.1f  st8x256 %.1f  st4x512 %.1f  st4x1024 %.1f  st2x1024 %.1f  st8x128 %.1f GB/s\n",
                alg / run<4, false>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
-               alg / run<8, false>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
                alg / run<4, true>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
-               alg / run<8, true>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6);
+               alg / run_st<4, 256>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
+               alg / run_st<8, 256>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
+               alg / run_st<4, 512>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
+               alg / run_st<4, 1024>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
+               alg / run_st<2, 1024>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
+               alg / run_st<8, 128>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6);
     }
     return 0;
 }
