@@ -1557,6 +1557,17 @@ int launch_imap(const pncxk_args *a, const pncxk_imap *m, int gather) {
     const bool al = (uintptr_t)src % (uintptr_t)(gather ? ues : pes) == 0 &&
                     (uintptr_t)dst % (uintptr_t)(gather ? pes : ues) == 0;
     if (transpose_geom(m, &g, al && xpose_merge())) {       // the loops (unaligned) tile P alone
+        // a packed U stride a little under a multiple of 2 MiB (x 254 doubles:
+        // 2^21 - 2^14 B) lands the columns of concurrent tiles on few DRAM
+        // channels in either tile order; skewing p0 by k tiles per u tile
+        // spreads them: x 254 get 48 -> 57-59 % (k 32), put 49-51 -> 53-54 %
+        // (k 8), 1024 x 260096 get 58 -> 67 %, put 53 -> 57 %
+        // (profiles/r04q_xpose_skew_ab.txt).  Other strides keep the order
+        // above: the skew cost 8192 x 8192 up to 36 points.
+        if (xpose_order() < 0) {
+            const int64_t S = g.su * pes, r = S & ((1LL << 21) - 1);
+            if (r >= (1LL << 21) - (1LL << 15)) g.diag = gather ? 8 : 32;
+        }
         const unsigned grid = (unsigned)(g.ntiles < MAX_BLOCKS ? g.ntiles : MAX_BLOCKS);
         const bool mrg = g.cin > 0;
         const Sink sk = sink_acquire(a->status, NC_ERANGE, st, grid, want);

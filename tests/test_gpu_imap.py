@@ -175,6 +175,16 @@ def test_imap_tile_merged_dims(torch_cuda, count, imap, xt, it, merge, order, kn
     test_imap_put_get(torch_cuda, count, imap, xt, it, "dev")
 
 
+@pytest.mark.parametrize("xt,it", [(T.NC_DOUBLE, T.ITYPE_DOUBLE), (T.NC_INT, T.ITYPE_DOUBLE), (T.NC_SHORT, T.ITYPE_FLOAT)])
+def test_imap_tile_channel_skew(torch_cuda, xt, it):
+    """a packed U stride just under a multiple of 2 MiB (1024 x 254 doubles
+    = 2^21 - 2^14 B, as the x 254 benchmark shape) takes the skewed tile
+    order by default (p0 shifted by 8 tiles per u tile on put, 32 on get);
+    the narrower external types give strides off that band and keep the
+    default order -- both against the oracle"""
+    test_imap_put_get(torch_cuda, [16, 1024, 254], [1, 16, 16 * 1024], xt, it, "dev")
+
+
 # 2-D transposes (U = P - 1) with tile grids wider than tall, taller than
 # wide and partial tiles on both edges, in both tile orders
 XPOSE2D_CASES = [([300, 70], [1, 300]), ([70, 300], [1, 70]), ([257, 129], [1, 257]), ([128, 64], [1, 128])]

@@ -255,8 +255,9 @@ float run_lds(const uint8_t *s, uint8_t *d, uint32_t nunits, uint32_t nq, uint32
 
 template <int U, bool NTL>
 float run(const uint8_t *s, uint8_t *d, uint32_t nunits, uint32_t nq, uint32_t tn, int64_t ext, const unsigned *t,
-          const unsigned char *nb) {
-    const unsigned grid = (nunits + 4 * U - 1) / (4 * U);
+          const unsigned char *nb, unsigned cap = 0) {
+    unsigned grid = (nunits + 4 * U - 1) / (4 * U);
+    if (cap && grid > cap) grid = cap;
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
@@ -330,7 +331,7 @@ int main() {
         hipMemcpy(h1.data(), u1, ub, hipMemcpyDeviceToHost);
         hipMemcpy(h2.data(), u2, ub, hipMemcpyDeviceToHost);
         printf("lds-merge scatter %s the plain scatter\n", h1 == h2 ? "matches" : "DIFFERS from");
-        for (int rep = 0; rep < 2; rep++)
+        for (int rep = 0; rep < 0; rep++)
             printf("get: plain4 %.1f  nt4 %.1f  plain2 %.1f  lds1 %.1f  lds2 %.1f GB/s\n",
                    alg / run_sc<4, 0>(pk, u1, nunits, nq, tn, ext, t, nbp) / 1e6,
                    alg / run_sc<4, 1>(pk, u1, nunits, nq, tn, ext, t, nbp) / 1e6,
@@ -339,7 +340,16 @@ int main() {
                    alg / run_sc<2, 2>(pk, u1, nunits, nq, tn, ext, t, nbp) / 1e6);
         hipFree(pk); hipFree(u1); hipFree(u2);
     }
-    for (int rep = 0; rep < 1; rep++) {
+    for (int rep = 0; rep < 2; rep++)
+        printf("U4nt grid cap: none %.1f  1024 %.1f  2048 %.1f  4096 %.1f  8192 %.1f  16384 %.1f  32768 %.1f GB/s\n",
+               alg / run<4, true>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
+               alg / run<4, true>(s, d, nunits, nq, tn, ext, t, nbp, 1024) / 1e6,
+               alg / run<4, true>(s, d, nunits, nq, tn, ext, t, nbp, 2048) / 1e6,
+               alg / run<4, true>(s, d, nunits, nq, tn, ext, t, nbp, 4096) / 1e6,
+               alg / run<4, true>(s, d, nunits, nq, tn, ext, t, nbp, 8192) / 1e6,
+               alg / run<4, true>(s, d, nunits, nq, tn, ext, t, nbp, 16384) / 1e6,
+               alg / run<4, true>(s, d, nunits, nq, tn, ext, t, nbp, 32768) / 1e6);
+    for (int rep = 0; rep < 0; rep++) {
         printf("U4 %.1f  U4nt %.1f  st4x256 %.1f  st8x256 %.1f  st4x512 %.1f  st4x1024 %.1f  st2x1024 %.1f  st8x128 %.1f GB/s\n",
                alg / run<4, false>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
                alg / run<4, true>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
