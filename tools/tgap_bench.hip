@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <random>
 #include <vector>
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -49,6 +50,223 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t *src, uint8_t *dst
         for (int i = 0; i < U; i++)
             if (ok[i]) __builtin_nontemporal_store(__builtin_bswap64(sv[i]), (uint64_t *)(dst + ko[i] * 8));
     }
+}
+
+// pairs: a lane moves elements 2p, 2p+1 of a 128-element pair of chunks
+// (lanes 0-31 the first chunk, 32-63 the second), one 16-byte store; the
+// gaps are a per-half prefix sum of the lane's two nibbles (one byte)
+__device__ __forceinline__ uint32_t half_inclusive_sum(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);
+    return v;
+}
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+template <int U>
+__global__ __launch_bounds__(256) void k_gather_pair(const uint8_t *src, uint8_t *dst, uint32_t npairs, uint32_t nq,
+                                                     uint32_t tn, int64_t textent, const unsigned *toff,
+                                                     const unsigned char *nib) {
+    // requires tn % 128 == 0 here (the probe layout is trimmed to that)
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, lp = lane & 31;
+    const uint32_t np = nq / 2;                       // pairs per copy
+    const uint32_t step = gridDim.x * 4 * U;
+    for (uint32_t u0 = blockIdx.x * 4 * U; u0 < npairs; u0 += step) {
+        uint64_t a[U], b[U];
+        int64_t ko[U];
+        bool ok[U];
+#pragma unroll
+        for (int i = 0; i < U; i++) {
+            uint32_t u = u0 + i * 4 + w;
+            const bool okw = u < npairs;
+            u = __builtin_amdgcn_readfirstlane(okw ? u : npairs - 1);
+            const uint32_t c = u / np, pr = u - c * np, q = 2 * pr + h;
+            ok[i] = okw;
+            const uint32_t by = nib[(int64_t)q * 32 + lp];
+            const uint32_t n0 = by & 15u, n1 = by >> 4;
+            const uint32_t P = half_inclusive_sum(n0 + n1);
+            const uint8_t *base = src + (int64_t)c * textent + toff[q];
+            const uint32_t e1 = 2 * lp + 1;
+            a[i] = __builtin_nontemporal_load((const uint64_t *)(base + (int64_t)(e1 - 1 + P - n1) * 8));
+            b[i] = __builtin_nontemporal_load((const uint64_t *)(base + (int64_t)(e1 + P) * 8));
+            ko[i] = (int64_t)c * tn + (int64_t)q * 64 + 2 * lp;
+        }
+#pragma unroll
+        for (int i = 0; i < U; i++)
+            if (ok[i]) {
+                u64x2 v = {__builtin_bswap64(a[i]), __builtin_bswap64(b[i])};
+                __builtin_nontemporal_store(v, (u64x2 *)(dst + ko[i] * 8));
+            }
+    }
+}
+
+template <int U>
+float run_pair(const uint8_t *s, uint8_t *d, uint32_t npairs, uint32_t nq, uint32_t tn, int64_t ext, const unsigned *t,
+               const unsigned char *nb) {
+    const unsigned grid = (npairs + 4 * U - 1) / (4 * U);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipLaunchKernelGGL((k_gather_pair<U>), dim3(grid), dim3(256), 0, 0, s, d, npairs, nq, tn, ext, t, nb);
+    hipEventRecord(a, 0);
+    for (int k = 0; k < 20; k++)
+        hipLaunchKernelGGL((k_gather_pair<U>), dim3(grid), dim3(256), 0, 0, s, d, npairs, nq, tn, ext, t, nb);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    return ms / 20;
+}
+
+// realign: the 4 waves of a block convert 4 consecutive chunks (256 packed
+// elements when they lie in one copy); the values go through LDS and are
+// stored from 64-element-aligned packed positions, so only the block's two
+// edge lines are partial instead of every wave's
+template <int U>
+__global__ __launch_bounds__(256) void k_gather_realign(const uint8_t *src, uint8_t *dst, uint32_t nunits, uint32_t nq,
+                                                        uint32_t tn, int64_t textent, const unsigned *toff,
+                                                        const unsigned char *nib) {
+    __shared__ uint64_t lv[U][256];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t step = gridDim.x * 4 * U;
+    for (uint32_t u0 = blockIdx.x * 4 * U; u0 < nunits; u0 += step) {
+        uint64_t sv[U];
+        int64_t ko[U];
+        bool ok[U];
+#pragma unroll
+        for (int i = 0; i < U; i++) {
+            uint32_t u = u0 + i * 4 + w;
+            const bool okw = u < nunits;
+            u = __builtin_amdgcn_readfirstlane(okw ? u : nunits - 1);
+            const uint32_t c = u / nq, q = u - c * nq, r = q * 64 + lane, rc = r < tn ? r : tn - 1;
+            ok[i] = okw && r < tn;
+            ko[i] = (int64_t)c * tn + rc;
+            const uint32_t b = nib[(int64_t)q * 32 + (lane >> 1)];
+            const uint32_t g = wave_inclusive_sum((b >> ((lane & 1) * 4)) & 15u);
+            const uint8_t *p = src + (int64_t)c * textent + toff[q] + (int64_t)((rc & 63) + g) * 8;
+            sv[i] = __builtin_nontemporal_load((const uint64_t *)p);
+        }
+#pragma unroll
+        for (int i = 0; i < U; i++) {
+            // the block's 4 chunks for this i: units ua..ua+3
+            const uint32_t ua = u0 + i * 4;
+            const uint32_t ca = ua / nq, qa = ua - ca * nq;
+            const bool whole = ua + 3 < nunits && qa + 3 < nq && (qa + 4) * 64 <= tn;   // 4 full chunks, one copy
+            if (whole) {
+                lv[i][threadIdx.x] = __builtin_bswap64(sv[i]);
+            } else if (ok[i]) {
+                __builtin_nontemporal_store(__builtin_bswap64(sv[i]), (uint64_t *)(dst + ko[i] * 8));
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < U; i++) {
+            const uint32_t ua = u0 + i * 4;
+            const uint32_t ca = ua / nq, qa = ua - ca * nq;
+            const bool whole = ua + 3 < nunits && qa + 3 < nq && (qa + 4) * 64 <= tn;
+            if (!whole) continue;
+            const int64_t p0 = (int64_t)ca * tn + (int64_t)qa * 64;      // first packed element of the 256
+            const int64_t a0 = p0 & ~63LL;
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const int64_t k = a0 + threadIdx.x + 256 * j;
+                if (k >= p0 && k < p0 + 256) __builtin_nontemporal_store(lv[i][k - p0], (uint64_t *)(dst + k * 8));
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <int U>
+float run_ra(const uint8_t *s, uint8_t *d, uint32_t nunits, uint32_t nq, uint32_t tn, int64_t ext, const unsigned *t,
+             const unsigned char *nb) {
+    const unsigned grid = (nunits + 4 * U - 1) / (4 * U);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipLaunchKernelGGL((k_gather_realign<U>), dim3(grid), dim3(256), 0, 0, s, d, nunits, nq, tn, ext, t, nb);
+    hipEventRecord(a, 0);
+    for (int k = 0; k < 20; k++)
+        hipLaunchKernelGGL((k_gather_realign<U>), dim3(grid), dim3(256), 0, 0, s, d, nunits, nq, tn, ext, t, nb);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    return ms / 20;
+}
+
+// packed-aligned windows: wave = packed elements [64u, 64u + 64), which may
+// span the tail of one map chunk, the next chunk and the next copy's first
+// chunk (up to 3 segments, tn >= 64).  One wave scan over the lanes'
+// nibbles gives the gaps inside each segment; the first segment also needs
+// the gaps before its first position in its chunk: a second scan of that
+// chunk's nibbles.  Stores are whole 512-byte runs at 64-element-aligned
+// packed positions.
+template <int U>
+__global__ __launch_bounds__(256) void k_gather_win(const uint8_t *src, uint8_t *dst, uint32_t nwin, uint32_t n,
+                                                    uint32_t tn, int64_t textent, const unsigned *toff,
+                                                    const unsigned char *nib) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t step = gridDim.x * 4 * U;
+    for (uint32_t u0 = blockIdx.x * 4 * U; u0 < nwin; u0 += step) {
+        uint64_t sv[U];
+        uint32_t kk[U];
+        bool ok[U];
+#pragma unroll
+        for (int i = 0; i < U; i++) {
+            uint32_t u = u0 + i * 4 + w;
+            const bool okw = u < nwin;
+            u = __builtin_amdgcn_readfirstlane(okw ? u : nwin - 1);
+            const uint32_t k0 = u * 64, c0 = k0 / tn, r0 = k0 - c0 * tn, q0 = r0 >> 6, p0 = r0 & 63;
+            const uint32_t bc = (c0 + 1) * tn - k0;                     // lanes left in copy c0
+            const uint32_t e0 = 64 - p0 < bc ? 64 - p0 : bc;            // end of segment 0
+            const bool s1copy = e0 == bc;                               // segment 1 starts copy c0 + 1
+            const uint32_t e1 = !s1copy && bc < 64 ? bc : 64;           // end of segment 1
+            uint32_t c, q, pos;
+            if (lane < e0) { c = c0; q = q0; pos = p0 + lane; }
+            else if (lane < e1) { c = s1copy ? c0 + 1 : c0; q = s1copy ? 0 : q0 + 1; pos = lane - e0; }
+            else { c = c0 + 1; q = 0; pos = lane - e1; }
+            const uint32_t k = k0 + lane;
+            ok[i] = okw && k < n;
+            kk[i] = k;
+            const uint32_t b = nib[(int64_t)q * 32 + (pos >> 1)];
+            const uint32_t S = wave_inclusive_sum((b >> ((pos & 1) * 4)) & 15u);
+            uint32_t m0 = 0;
+            if (p0 != 0) {
+                const uint32_t b0 = nib[(int64_t)q0 * 32 + (lane >> 1)];
+                const uint32_t T = wave_inclusive_sum((b0 >> ((lane & 1) * 4)) & 15u);
+                m0 = __builtin_amdgcn_readlane(T, p0 - 1);
+            }
+            const uint32_t s0 = __builtin_amdgcn_readlane(S, e0 - 1);
+            const uint32_t s1 = __builtin_amdgcn_readlane(S, (e1 < 64 ? e1 : 64) - 1);
+            const uint32_t g = lane < e0 ? m0 + S : lane < e1 ? S - s0 : S - s1;
+            const uint8_t *p = ok[i] ? src + (int64_t)c * textent + toff[q] + (int64_t)(pos + g) * 8 : src;
+            sv[i] = __builtin_nontemporal_load((const uint64_t *)p);
+        }
+#pragma unroll
+        for (int i = 0; i < U; i++)
+            if (ok[i]) __builtin_nontemporal_store(__builtin_bswap64(sv[i]), (uint64_t *)(dst + (int64_t)kk[i] * 8));
+    }
+}
+
+template <int U>
+float run_win(const uint8_t *s, uint8_t *d, uint32_t n, uint32_t tn, int64_t ext, const unsigned *t,
+              const unsigned char *nb) {
+    const uint32_t nwin = (n + 63) / 64;
+    const unsigned grid = (nwin + 4 * U - 1) / (4 * U);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipLaunchKernelGGL((k_gather_win<U>), dim3(grid), dim3(256), 0, 0, s, d, nwin, n, tn, ext, t, nb);
+    hipEventRecord(a, 0);
+    for (int k = 0; k < 20; k++)
+        hipLaunchKernelGGL((k_gather_win<U>), dim3(grid), dim3(256), 0, 0, s, d, nwin, n, tn, ext, t, nb);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    return ms / 20;
 }
 
 // staged: every unit's map loads first, then the scans, then the element
@@ -283,6 +501,7 @@ int main() {
         for (int e = 0; e < len; e++) o.push_back((unsigned)((pos + e) * 8));
         pos += len + gap;
     }
+    if (getenv("TRIM")) o.resize(o.size() / 128 * 128);   // whole chunk pairs (k_gather_pair)
     const uint32_t tn = (uint32_t)o.size(), nq = (tn + 63) / 64, nunits = nq * copies;
     const int64_t ext = (int64_t)pos * 8;
     std::vector<unsigned> base(nq);
@@ -306,11 +525,11 @@ int main() {
         uint8_t *d2;
         if (hipMalloc(&d2, (size_t)tn * copies * 8)) return 4;
         run<4, false>(s, d, nunits, nq, tn, ext, t, nbp);
-        run_st<4, 256>(s, d2, nunits, nq, tn, ext, t, nbp);
+        run_win<4>(s, d2, tn * copies, tn, ext, t, nbp);
         std::vector<uint8_t> h1((size_t)tn * copies * 8), h2(h1.size());
         hipMemcpy(h1.data(), d, h1.size(), hipMemcpyDeviceToHost);
         hipMemcpy(h2.data(), d2, h2.size(), hipMemcpyDeviceToHost);
-        printf("staged variant %s the plain gather\n", h1 == h2 ? "matches" : "DIFFERS from");
+        printf("window variant %s the plain gather\n", h1 == h2 ? "matches" : "DIFFERS from");
         hipFree(d2);
     }
     {
@@ -341,6 +560,12 @@ int main() {
         hipFree(pk); hipFree(u1); hipFree(u2);
     }
     for (int rep = 0; rep < 2; rep++)
+        printf("tn %u (tn %% 64 = %u): U4nt %.1f  win2 %.1f  win4 %.1f  win8 %.1f GB/s\n", tn, tn % 64,
+               alg / run<4, true>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
+               alg / run_win<2>(s, d, tn * copies, tn, ext, t, nbp) / 1e6,
+               alg / run_win<4>(s, d, tn * copies, tn, ext, t, nbp) / 1e6,
+               alg / run_win<8>(s, d, tn * copies, tn, ext, t, nbp) / 1e6);
+    for (int rep = 0; rep < 0; rep++)
         printf("U4nt grid cap: none %.1f  1024 %.1f  2048 %.1f  4096 %.1f  8192 %.1f  16384 %.1f  32768 %.1f GB/s\n",
                alg / run<4, true>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
                alg / run<4, true>(s, d, nunits, nq, tn, ext, t, nbp, 1024) / 1e6,
