@@ -205,6 +205,27 @@ def test_flex_offset_map_widths(torch_cuda, where, map16, gap, tgap, knob):
     run_case(torch_cuda, where, T.NC_INT, T.ITYPE_INT, [9, 0, 20, 3, 40], [2, 1, 5, 1, 3], 50, 4, [12, 4], [1, 12], 22)
 
 
+GAP_SHAPES = [
+    ([0, 3, 9], [2, 1, 3], 14, 300),                 # tn 6 < one chunk, many copies
+    (list(range(0, 128, 2)), [1] * 64, 130, 7),      # tn exactly 64, every other element
+    (list(range(0, 130, 2)), [1] * 65, 131, 5),      # tn 65: a one-element second chunk
+    ([0, 30, 62], [15, 17, 10], 80, 9),              # gaps of exactly 15 elements fit the nibbles
+]
+
+
+@pytest.mark.parametrize("where", ["host", "dev"])
+@pytest.mark.parametrize("shape", range(len(GAP_SHAPES)))
+@pytest.mark.parametrize("xt,it", [(T.NC_SHORT, T.ITYPE_INT), (T.NC_INT, T.ITYPE_SCHAR), (T.NC_DOUBLE, T.ITYPE_DOUBLE)])
+def test_flex_gap_map_edges(torch_cuda, where, shape, xt, it, knob):
+    """the 4-bit map on k_tgap at its edges: typemaps shorter than a chunk
+    with hundreds of copies, exactly one chunk, one chunk and one element,
+    gaps of exactly 15 elements; NC_ERANGE both ways (int -> NC_SHORT on put,
+    NC_INT -> schar on get) and a plain swap; against the oracle"""
+    knob("TOFF16", "-1")
+    disp, blen, ext, bufcount = GAP_SHAPES[shape]
+    run_case(torch_cuda, where, xt, it, disp, blen, ext, bufcount, None, None, 50 + shape)
+
+
 @pytest.mark.parametrize("where", ["host", "dev"])
 @pytest.mark.parametrize("map16", ["-1", "8"], ids=["map4", "map8"])
 def test_flex_gap_map_through_imap(torch_cuda, where, map16, knob):
