@@ -471,6 +471,61 @@ float run_lds(const uint8_t *s, uint8_t *d, uint32_t nunits, uint32_t nq, uint32
     return ms / 20;
 }
 
+// store policy on the packed side: 0 nt (as k_gather), 1 plain write-back,
+// 2 nt sc1 (st_stream in the library), with nontemporal user-side loads
+template <int U, int SP>
+__global__ __launch_bounds__(256) void k_gather_sp(const uint8_t *src, uint8_t *dst, uint32_t nunits, uint32_t nq,
+                                                   uint32_t tn, int64_t textent, const unsigned *toff,
+                                                   const unsigned char *nib) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t step = gridDim.x * 4 * U;
+    for (uint32_t u0 = blockIdx.x * 4 * U; u0 < nunits; u0 += step) {
+        uint64_t sv[U];
+        int64_t ko[U];
+        bool ok[U];
+#pragma unroll
+        for (int i = 0; i < U; i++) {
+            uint32_t u = u0 + i * 4 + w;
+            const bool okw = u < nunits;
+            u = __builtin_amdgcn_readfirstlane(okw ? u : nunits - 1);
+            const uint32_t c = u / nq, q = u - c * nq, r = q * 64 + lane, rc = r < tn ? r : tn - 1;
+            ok[i] = okw && r < tn;
+            ko[i] = (int64_t)c * tn + rc;
+            const uint32_t b = nib[(int64_t)q * 32 + (lane >> 1)];
+            const uint32_t g = wave_inclusive_sum((b >> ((lane & 1) * 4)) & 15u);
+            const uint8_t *p = src + (int64_t)c * textent + toff[q] + (int64_t)((rc & 63) + g) * 8;
+            sv[i] = __builtin_nontemporal_load((const uint64_t *)p);
+        }
+#pragma unroll
+        for (int i = 0; i < U; i++)
+            if (ok[i]) {
+                uint64_t *p = (uint64_t *)(dst + ko[i] * 8);
+                const uint64_t v = __builtin_bswap64(sv[i]);
+                if constexpr (SP == 0) __builtin_nontemporal_store(v, p);
+                else if constexpr (SP == 1) *p = v;
+                else asm volatile("global_store_dwordx2 %0, %1, off nt sc1" ::"v"(p), "v"(v) : "memory");
+            }
+    }
+}
+
+template <int U, int SP>
+float run_sp(const uint8_t *s, uint8_t *d, uint32_t nunits, uint32_t nq, uint32_t tn, int64_t ext, const unsigned *t,
+             const unsigned char *nb) {
+    const unsigned grid = (nunits + 4 * U - 1) / (4 * U);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipLaunchKernelGGL((k_gather_sp<U, SP>), dim3(grid), dim3(256), 0, 0, s, d, nunits, nq, tn, ext, t, nb);
+    hipEventRecord(a, 0);
+    for (int k = 0; k < 20; k++)
+        hipLaunchKernelGGL((k_gather_sp<U, SP>), dim3(grid), dim3(256), 0, 0, s, d, nunits, nq, tn, ext, t, nb);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    return ms / 20;
+}
+
 template <int U, bool NTL>
 float run(const uint8_t *s, uint8_t *d, uint32_t nunits, uint32_t nq, uint32_t tn, int64_t ext, const unsigned *t,
           const unsigned char *nb, unsigned cap = 0) {
@@ -525,11 +580,11 @@ int main() {
         uint8_t *d2;
         if (hipMalloc(&d2, (size_t)tn * copies * 8)) return 4;
         run<4, false>(s, d, nunits, nq, tn, ext, t, nbp);
-        run_win<4>(s, d2, tn * copies, tn, ext, t, nbp);
+        run_sp<4, 1>(s, d2, nunits, nq, tn, ext, t, nbp);
         std::vector<uint8_t> h1((size_t)tn * copies * 8), h2(h1.size());
         hipMemcpy(h1.data(), d, h1.size(), hipMemcpyDeviceToHost);
         hipMemcpy(h2.data(), d2, h2.size(), hipMemcpyDeviceToHost);
-        printf("window variant %s the plain gather\n", h1 == h2 ? "matches" : "DIFFERS from");
+        printf("write-back store variant %s the plain gather\n", h1 == h2 ? "matches" : "DIFFERS from");
         hipFree(d2);
     }
     {
@@ -560,11 +615,12 @@ int main() {
         hipFree(pk); hipFree(u1); hipFree(u2);
     }
     for (int rep = 0; rep < 2; rep++)
-        printf("tn %u (tn %% 64 = %u): U4nt %.1f  win2 %.1f  win4 %.1f  win8 %.1f GB/s\n", tn, tn % 64,
-               alg / run<4, true>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
-               alg / run_win<2>(s, d, tn * copies, tn, ext, t, nbp) / 1e6,
-               alg / run_win<4>(s, d, tn * copies, tn, ext, t, nbp) / 1e6,
-               alg / run_win<8>(s, d, tn * copies, tn, ext, t, nbp) / 1e6);
+        printf("tn %u (tn %% 64 = %u): store nt %.1f  write-back %.1f  nt sc1 %.1f | U2: nt %.1f  wb %.1f GB/s\n", tn, tn % 64,
+               alg / run_sp<4, 0>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
+               alg / run_sp<4, 1>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
+               alg / run_sp<4, 2>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
+               alg / run_sp<2, 0>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
+               alg / run_sp<2, 1>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6);
     for (int rep = 0; rep < 0; rep++)
         printf("U4nt grid cap: none %.1f  1024 %.1f  2048 %.1f  4096 %.1f  8192 %.1f  16384 %.1f  32768 %.1f GB/s\n",
                alg / run<4, true>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
