@@ -603,19 +603,97 @@ def c1_reference_sequence(path, var_offset, reps=21, n=1 << 20):
     lib.orc_c1_sequence.argtypes = [ctypes.c_char_p, ctypes.c_longlong, ctypes.c_longlong, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
     lib.orc_c1_sequence.restype = ctypes.c_int
-    pm, gm = ctypes.c_double(0), ctypes.c_double(0)
-    rc = lib.orc_c1_sequence(path.encode(), var_offset, n, reps, ctypes.byref(pm), ctypes.byref(gm))
-    put_ms, get_ms = pm.value, gm.value
+    pm, gm = ctypes.c_double(0), (ctypes.c_double * 2)()
+    rc = lib.orc_c1_sequence(path.encode(), var_offset, n, reps, ctypes.byref(pm), gm)
+    put_ms, get_ms = pm.value, gm[0]
     xbytes = 4.0 * n
     out = {"unit": "GiB/s", "cores": 1, "kind": "port", "check_ok": rc == 0,
            "sample": f"the whole C1 request ({n} NC_INT, 4 MiB) on the same tmpfs file, median of {reps}: "
-                     f"oracle restatement of the reference loop timed in C (oracle/ref_sequence.c): "
-                     f"orc_in_swapn + pwrite + orc_in_swapn back / pread + orc_in_swapn, 1 thread"}
+                     f"oracle restatement of the reference loop timed in C (oracle/ref_sequence.c), 1 thread: "
+                     f"put = orc_in_swapn of the user buffer + pwrite + orc_in_swapn back; get = malloc xbuf + "
+                     f"pread into it + orc_in_swapn + memcpy into the user buffer + free "
+                     f"(ncmpio_getput.m4:415-427,468-470, ncmpio_util.c:884-888,934-936)"}
     if rc == 0:
         out.update({"value": round(2 * xbytes / ((put_ms + get_ms) * 1e-3) / GIB, 3),
-                    "put_ms": round(put_ms, 4), "get_ms": round(get_ms, 4)})
+                    "put_ms": round(put_ms, 4), "get_ms": round(get_ms, 4),
+                    "get_ms_read_into_user_and_swap": round(gm[1], 4)})
     else:
         out["error"] = rc
+    return out
+
+
+def c1_first_touch(nrec=32, n=1 << 20, cpu=True):
+    """C1 under the reference's own benchmark pattern
+    (benchmarks/C/pnetcdf_put_vara.c:193-209): a record variable x(time, n)
+    NC_INT, each 4 MiB record put exactly once with ncmpi_put_vara_int_all
+    (appended past the end of the file) and then got once
+    (tests/mpi/api_check c1first), per-call medians; beside it the
+    reference's sequence on the same records in the same run
+    (oracle/ref_sequence.c orc_c1_first_sequence: swap, pwrite, swap back,
+    numrecs; malloc xbuf, pread, swap, memcpy, free), timed before and after
+    the library's legs."""
+    exe = os.path.join(ROOT, "tests", "mpi", "api_check")
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
+    path = os.path.join(shm, f"pncx_c1first_{os.getpid()}.nc")
+    xbytes = 4.0 * n
+    legs, refs, rec_offset = {}, [], None
+
+    def ref_run():
+        from oracle import oracle as O
+        lib = O.lib()
+        lib.orc_c1_first_sequence.argtypes = [ctypes.c_char_p, ctypes.c_longlong, ctypes.c_longlong, ctypes.c_int,
+                                              ctypes.POINTER(ctypes.c_double)]
+        lib.orc_c1_first_sequence.restype = ctypes.c_int
+        o = (ctypes.c_double * 6)()
+        rc = lib.orc_c1_first_sequence(path.encode(), rec_offset, n, nrec, o)
+        return {"check_ok": rc == 0, "error": rc} if rc else {
+            "check_ok": True, "put_ms": round(o[0], 4), "get_ms": round(o[1], 4), "put_ms_min": round(o[2], 4),
+            "get_ms_min": round(o[3], 4), "put_loop_ms": round(o[4], 3), "get_loop_ms": round(o[5], 3)}
+
+    order = [("host_8_io_threads", 0, None), ("ref", None, None), ("host_1_io_thread", 0, "1"),
+             ("device_buffers", 1, None), ("ref", None, None)]
+    for key, dev, threads in order:
+        if key == "ref":
+            if cpu and rec_offset is not None:
+                refs.append(ref_run())
+            continue
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if threads is not None:
+            env["PNCX_IO_THREADS"] = threads
+        r = subprocess.run([exe, "c1first", path, str(n), str(nrec), str(dev)], capture_output=True, text=True,
+                           timeout=300, env=env)
+        if r.returncode != 0:
+            legs[key] = {"error": r.returncode, "stderr": r.stderr[-400:]}
+            continue
+        o = json.loads(r.stdout.strip().splitlines()[-1])
+        rec_offset = o["rec_offset"]
+        legs[key] = {"put_ms": o["put_ms_median"], "get_ms": o["get_ms_median"], "put_ms_min": o["put_ms_min"],
+                     "get_ms_min": o["get_ms_min"], "put_loop_ms": o["put_loop_ms"], "get_loop_ms": o["get_loop_ms"],
+                     "close_ms": o["close_ms"], "errors": o["errors"],
+                     "put_GiBps": round(xbytes / (o["put_ms_median"] * 1e-3) / GIB, 3),
+                     "get_GiBps": round(xbytes / (o["get_ms_median"] * 1e-3) / GIB, 3)}
+    out = {"pattern": f"benchmarks/C/pnetcdf_put_vara.c:193-209, one rank: record variable x(time, {n}) NC_INT, "
+                      f"{nrec} records of 4 MiB each put once (appended) then got once; per-call medians",
+           "legs": legs}
+    if refs:
+        ok = [x for x in refs if x.get("check_ok")]
+        out["reference_sequence"] = {"runs": refs, "cores": 1, "kind": "port",
+                                     "sample": "oracle/ref_sequence.c orc_c1_first_sequence on the same file and "
+                                               "records, timed before and after the library's legs"}
+        if ok:
+            rp = sum(x["put_ms"] for x in ok) / len(ok)
+            rg = sum(x["get_ms"] for x in ok) / len(ok)
+            out["reference_sequence"].update({"put_ms": round(rp, 4), "get_ms": round(rg, 4)})
+            for key, leg in legs.items():
+                if "put_ms" in leg:
+                    leg["put_vs_reference"] = round(rp / leg["put_ms"], 3)
+                    leg["get_vs_reference"] = round(rg / leg["get_ms"], 3)
+    out["check_ok"] = all(v.get("errors", 1) == 0 for v in legs.values()) and all(x.get("check_ok") for x in refs)
+    try:
+        os.unlink(path)
+    except OSError:
+        pass
     return out
 
 
@@ -636,11 +714,12 @@ def c1_workload(cpu=True):
     if cpu and "var_offset" in res:
         out["cpu_baseline"] = c1_reference_sequence(path, res["var_offset"])
         ok = ok and out["cpu_baseline"]["check_ok"]
-    out["check_ok"] = ok
     try:
         os.unlink(path)
     except OSError:
         pass
+    res["first_touch"] = c1_first_touch(cpu=cpu)
+    out["check_ok"] = ok and res["first_touch"]["check_ok"]
     return out
 
 

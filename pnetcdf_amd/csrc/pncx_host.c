@@ -100,12 +100,13 @@ static const char *const g_ph_names[PH_N] = {
     "put.plan", "put.register", "put.convert", "put.write", "put.wait", "put.unregister", "put.total",
     "get.plan", "get.register", "get.read", "get.convert", "get.unregister", "get.total",
     "conv.lock_pin", "conv.enqueue", "conv.sync", "conv.status", "conv.unpin",
-    "gpu.h2d", "gpu.kernel", "gpu.d2h", "file.window_map", "file.window_use"};
+    "gpu.h2d", "gpu.kernel", "gpu.d2h", "file.window_map", "file.window_use", "put.grow"};
 
 /* A/B knobs (pncx_shim.h): the environment once at load, then pncx_knob_set */
 static const char *const g_knob_names[PNCXK_NKNOB] = {
     "TILE_U", "XPOSE_MERGE", "URUN", "TMAP_VEC", "IMAP_ROWS", "FUSE_LANES", "BATCH_FUSE", "TMAP_IMAP",
-    "TOFF16", "TOFF_MAX_ELEMS", "XPOSE_ORDER", "TOFF_RUNS", "HOST_ZC", "IO_INLINE_MB", "FILE_WINDOW", "IO_POPULATE", "HOST_ZC_MAX_MB", "TGAP"};
+    "TOFF16", "TOFF_MAX_ELEMS", "XPOSE_ORDER", "TOFF_RUNS", "HOST_ZC", "IO_INLINE_MB", "FILE_WINDOW", "IO_POPULATE", "HOST_ZC_MAX_MB", "TGAP",
+    "GROW", "READ_SPLIT"};
 static long long g_knob[PNCXK_NKNOB];
 
 long long pncx_knob(int id)
@@ -591,7 +592,35 @@ struct pncx_stage {
     int err;
     pinned_t pn;
     int ph_ev;
+    /* device-accessible host ranges resolved once per call (pncx_stage_hint):
+     * a push inside one of them needs no runtime lookup (two pointer-attribute
+     * and two device-pointer queries per side and chunk otherwise, 40-50 us
+     * per 4-chunk call on some hosts) */
+    struct { const char *h; size_t n; char *d; } hint[4];
+    int nhint;
 };
+
+/* device address of host range [p, p + n), from the call's hints or the runtime */
+static void *stage_dptr(pncx_stage *h, const void *p, size_t n)
+{
+    int i;
+    for (i = 0; i < h->nhint; i++)
+        if ((const char *)p >= h->hint[i].h && (const char *)p + n <= h->hint[i].h + h->hint[i].n)
+            return h->hint[i].d + ((const char *)p - h->hint[i].h);
+    return pncxrt_host_dptr_range(p, n);
+}
+
+/* the caller's whole host buffer (or staging area), resolved once */
+void pncx_stage_hint(pncx_stage *h, const void *p, size_t n)
+{
+    char *d;
+    if (h == NULL || p == NULL || n == 0 || h->nhint >= 4) return;
+    if ((d = (char *)pncxrt_host_dptr_range(p, n)) == NULL) return;
+    h->hint[h->nhint].h = (const char *)p;
+    h->hint[h->nhint].n = n;
+    h->hint[h->nhint].d = d;
+    h->nhint++;
+}
 
 static int stage_slots(ctx_t *c, size_t slot_bytes)
 {
@@ -722,11 +751,16 @@ int pncx_stage_push(pncx_stage *h, const void *src, void *dst, long long n)
     if (pncx_ph_on > 1 && c->pev[4 * PH_EVCH - 1] && h->ph_ev < PH_EVCH) ev = &c->pev[4 * h->ph_ev++];
     if ((h->mode == STAGE_ZCOUT || h->mode == STAGE_ZC) && !(op->kind == PNCXK_SWAP && op->a == 1)) {
         /* zero-copy: the kernel writes the host destination itself */
-        void *ddst = pncxrt_host_dptr_range(dst, (size_t)n * op->ds);
-        const void *dsrc = h->mode == STAGE_ZC ? pncxrt_host_dptr_range(src, (size_t)n * op->ss) : NULL;
+        void *ddst = stage_dptr(h, dst, (size_t)n * op->ds);
+        const void *dsrc = h->mode == STAGE_ZC ? stage_dptr(h, src, (size_t)n * op->ss) : NULL;
         if (ddst != NULL && h->mode == STAGE_ZC && dsrc != NULL) {
             void *q = c->stream[k & 1];
+            /* no copies: gpu.h2d and gpu.d2h read 0, gpu.kernel the kernel */
+            if (!err && ev) err = pncxrt_event_record(ev[0], q);
+            if (!err && ev) err = pncxrt_event_record(ev[1], q);
             if (!err) err = launch_op(op, dsrc, ddst, n, h->want_status ? c->dstatus : NULL, q);
+            if (!err && ev) err = pncxrt_event_record(ev[2], q);
+            if (!err && ev) err = pncxrt_event_record(ev[3], q);
             if (!err) err = pncxrt_event_record(c->sev_out[e], q);
             PH_ADD(PH_CONV_ENQUEUE, t0);
             if (err) return h->err = err < 0 ? err : PNCX_EDEVICE;
@@ -857,7 +891,7 @@ long long pncx_stage_chunk(const pncx_stage *h) { return h->chunk; }
  * registered host memory, a registered file window), waited for.  Returns
  * the status (NC_ERANGE) or an error. */
 int pncx_direct_convert(int dir, int cdf_ver, int xtype, int itype, const void *fillp, const void *dsrc,
-                        void *ddst, long long n)
+                        void *ddst, long long n, void *const *after)
 {
     op_t op;
     ctx_t *c;
@@ -875,6 +909,12 @@ int pncx_direct_convert(int dir, int cdf_ver, int xtype, int itype, const void *
     want = op.kind != PNCXK_SWAP;
     pthread_mutex_lock(&c->lock);
     err = stage_slots(c, 0);                      /* the events and the pinned status word */
+    if (!err && after != NULL) {
+        /* a device buffer the caller's stream produces (put) or still reads
+         * (get): the launch follows everything queued there before the call */
+        err = pncxrt_event_record(c->sev_init, *after);
+        if (!err) err = pncxrt_stream_wait_event(c->stream[0], c->sev_init);
+    }
     if (!err && want) err = pncxrt_memset(c->dstatus, 0, sizeof(int), c->stream[0]);
     if (!err) err = launch_op(&op, dsrc, ddst, n, want ? c->dstatus : NULL, c->stream[0]);
     if (!err && want) err = pncxrt_memcpy_d2h(c->hstat, c->dstatus, sizeof(int), c->stream[0]);
@@ -910,6 +950,10 @@ static int host_staged(const op_t *op, const void *src, void *dst, long long n, 
     if (alt) h->mode = STAGE_ALT;
     pin_range(&h->pn, src, (size_t)n * op->ss);
     pin_range(&h->pn, dst, (size_t)n * op->ds);
+    if (h->mode == STAGE_ZC || h->mode == STAGE_ZCOUT) {
+        pncx_stage_hint(h, src, (size_t)n * op->ss);
+        if (dst != src) pncx_stage_hint(h, dst, (size_t)n * op->ds);
+    }
     for (off = 0; off < n; off += chunk) {
         const long long m = n - off < chunk ? n - off : chunk;
         const int k = pncx_stage_push(h, (const uint8_t *)src + (size_t)off * op->ss,

@@ -284,32 +284,12 @@ void pio_batch_destroy(pio_batch *b)
     pthread_cond_destroy(&b->c);
 }
 
-int pio_submit(pio_batch *b, int fd, int write, const pio_run *runs, size_t n)
+/* queue the job as nt tasks of about equal byte ranges */
+static int queue_tasks(pio_batch *b, int fd, int write, const pio_run *runs, size_t n, long long total, int nt)
 {
-    long long total = 0, per;
-    size_t i;
-    int nt, tasks, k, *refs;
+    long long per;
+    int k, *refs;
     pio_run *copy;
-    for (i = 0; i < n; i++) total += runs[i].len;
-    if (total == 0) return NC_NOERR;
-    nt = total < INLINE_BYTES ? 0 : pio_threads();
-    tasks = nt;
-    if ((long long)tasks * MIN_TASK_BYTES > total) tasks = (int)(total / MIN_TASK_BYTES);
-    if (tasks < 1) tasks = 1;
-    /* one writer: pwrite (4 MiB on the MI355X host: 108 us, against 514 us
-     * through a mapping and 174 us with MAP_POPULATE, tools/c1_probe.hip);
-     * mappings only when several tasks write one file at once */
-    if (write) write = (nt <= 1 || tasks <= 1) ? 1 : write_mode(fd, runs, n, total);
-    if (nt <= 1) {
-        const int err = do_range(fd, write, runs, n, 0, total);
-        if (err) {
-            pthread_mutex_lock(&b->m);
-            if (!b->err) b->err = err;
-            pthread_mutex_unlock(&b->m);
-        }
-        return err;
-    }
-    nt = tasks;
     copy = (pio_run *)malloc(sizeof(pio_run) * n);
     refs = (int *)malloc(sizeof(int));
     if (copy == NULL || refs == NULL) { free(copy); free(refs); return NC_ENOMEM; }
@@ -341,6 +321,57 @@ int pio_submit(pio_batch *b, int fd, int write, const pio_run *runs, size_t n)
         pthread_mutex_unlock(&q_lock);
     }
     return NC_NOERR;
+}
+
+int pio_submit(pio_batch *b, int fd, int write, const pio_run *runs, size_t n)
+{
+    long long total = 0;
+    size_t i;
+    int nt, tasks;
+    for (i = 0; i < n; i++) total += runs[i].len;
+    if (total == 0) return NC_NOERR;
+    nt = total < INLINE_BYTES ? 0 : pio_threads();
+    tasks = nt;
+    if ((long long)tasks * MIN_TASK_BYTES > total) tasks = (int)(total / MIN_TASK_BYTES);
+    if (tasks < 1) tasks = 1;
+    /* one writer: pwrite (4 MiB on the MI355X host: 108 us, against 514 us
+     * through a mapping and 174 us with MAP_POPULATE, tools/c1_probe.hip);
+     * mappings only when several tasks write one file at once */
+    if (write) write = (nt <= 1 || tasks <= 1) ? 1 : write_mode(fd, runs, n, total);
+    if (nt <= 1) {
+        const int err = do_range(fd, write, runs, n, 0, total);
+        if (err) {
+            pthread_mutex_lock(&b->m);
+            if (!b->err) b->err = err;
+            pthread_mutex_unlock(&b->m);
+        }
+        return err;
+    }
+    return queue_tasks(b, fd, write, runs, n, total, tasks);
+}
+
+/* Reads of a small job spread over `parts` pool threads (pread of one
+ * tmpfs file takes no exclusive lock, so the copies run side by side);
+ * pieces of at least 64 KiB. */
+int pio_read_split(pio_batch *b, int fd, const pio_run *runs, size_t n, int parts)
+{
+    long long total = 0;
+    size_t i;
+    int nt = pio_threads();
+    for (i = 0; i < n; i++) total += runs[i].len;
+    if (total == 0) return NC_NOERR;
+    if (parts > nt) parts = nt;
+    if ((long long)parts * (64 << 10) > total) parts = (int)(total / (64 << 10));
+    if (parts < 2) {
+        const int err = do_range(fd, 0, runs, n, 0, total);
+        if (err) {
+            pthread_mutex_lock(&b->m);
+            if (!b->err) b->err = err;
+            pthread_mutex_unlock(&b->m);
+        }
+        return err;
+    }
+    return queue_tasks(b, fd, 0, runs, n, total, parts);
 }
 
 int pio_wait(pio_batch *b)

@@ -41,6 +41,10 @@ int  pio_rw_inline(int fd, int write, const pio_run *runs, size_t n);
 /* Synchronous convenience: submit + wait. */
 int  pio_rw(int fd, int write, const pio_run *runs, size_t n);
 int  pio_threads(void);
+/* A read job split over up to `parts` pool threads whatever its size
+ * (pieces of at least 64 KiB): the inline gets' chunks (pncx_nc.c). */
+int  pio_read_split(pio_batch *b, int fd, const pio_run *runs, size_t n, int parts);
+
 
 int  pio_write_all(int fd, const void *buf, size_t n, long long off);
 int  pio_read_all(int fd, void *buf, size_t n, long long off);

@@ -584,12 +584,28 @@ int pncxrt_host_register_map(void *p, size_t n, int readonly) {
     return PNCX_EDEVICE;
 }
 void *pncxrt_host_dptr_range(const void *p, size_t n) {
-    /* the device address of [p, p + n) when the whole range is pinned or
-     * registered host memory mapped linearly (its first and last bytes
-     * translate n - 1 apart), else NULL: a range that starts inside one
-     * registration and runs past its end must not reach a kernel */
+    /* the device address of [p, p + n) when the whole range lies inside ONE
+     * pinned or registered host allocation, else NULL: a range that starts
+     * inside one registration and runs past its end, or spans two
+     * registrations with pageable memory between them, must not reach a
+     * kernel.  The runtime's range of the allocation holding p
+     * (HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR / _SIZE: the registration
+     * itself for hipHostRegister'ed memory, tools/ptr_range_probe.hip,
+     * profiles/r05b_ptr_range_probe.txt) must contain the whole range.
+     * Where the runtime reports no range (not seen on ROCm 7.2), the weaker
+     * check remains: the first and last bytes translate n - 1 apart, which
+     * two registrations with a pageable gap between them can also pass. */
     char *a = (char *)pncxrt_host_dptr(p);
     if (a == nullptr || n == 0) return a;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&base, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) == hipSuccess &&
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) == hipSuccess &&
+        base != nullptr && size > 0) {
+        const char *lo = (const char *)base, *q = (const char *)p;
+        return q >= lo && q + n <= lo + size ? a : nullptr;
+    }
+    (void)hipGetLastError();
     char *b = (char *)pncxrt_host_dptr((const char *)p + (n - 1));
     return b == a + (n - 1) ? a : nullptr;
 }

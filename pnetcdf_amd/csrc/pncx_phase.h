@@ -34,6 +34,7 @@ enum {
     PH_GPU_D2H,
     PH_WIN_MAP,         /* a file window mapped and registered             */
     PH_WIN_USE,         /* a request converted through a file window       */
+    PH_PUT_GROW,        /* appended pages allocated while the GPU converts */
     PH_N
 };
 

@@ -181,6 +181,9 @@ enum {
     PNCXK_KNOB_IO_POPULATE,     /* 0: mapped writes fault their pages in     */
     PNCXK_KNOB_HOST_ZC_MAX_MB,  /* largest call given zero-copy chunks       */
     PNCXK_KNOB_TGAP,            /* 0: 8-bit gap maps stay on k_imap          */
+    PNCXK_KNOB_GROW,            /* 0: no fallocate of appended ranges while
+                                 * the GPU converts (tmpfs)                  */
+    PNCXK_KNOB_READ_SPLIT,      /* pool preads per chunk of an inline get    */
     PNCXK_NKNOB
 };
 long long pncx_knob(int id);

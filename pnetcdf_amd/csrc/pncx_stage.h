@@ -32,12 +32,18 @@ int pncx_stage_push(pncx_stage *h, const void *src, void *dst, long long nelems)
 int pncx_stage_wait(pncx_stage *h, int k);
 int pncx_stage_end(pncx_stage *h);
 long long pncx_stage_chunk(const pncx_stage *h);
+/* [p, p + n) is one device-accessible host range for the rest of the call
+ * (the registered user buffer, the pinned staging area): pushes inside it
+ * skip the runtime's pointer lookups */
+void pncx_stage_hint(pncx_stage *h, const void *p, size_t n);
 
 /* one conversion launch between device-accessible pointers (HBM, pinned or
  * registered host memory, a registered file window), waited for: the
- * status (NC_ERANGE) or an error */
+ * status (NC_ERANGE) or an error.  after: NULL, or the address of a stream
+ * handle (the caller's; a NULL handle is the legacy default stream) whose
+ * queued work the launch must follow */
 int pncx_direct_convert(int dir, int cdf_ver, int xtype, int itype, const void *fillp, const void *dsrc,
-                        void *ddst, long long nelems);
+                        void *ddst, long long nelems, void *const *after);
 
 #ifdef __cplusplus
 }

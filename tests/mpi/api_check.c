@@ -15,6 +15,13 @@
  *       config 1 timed: reps x ncmpi_put_vara_int_all, then reps x
  *       ncmpi_get_vara_int_all of 1-D NC_INT x(n) on one open file (host or
  *       hipMalloc'ed buffers); prints median/min ms and the variable's offset.
+ *   api_check c1first <nc> <n> <nrec> <dev>
+ *       config 1 under benchmarks/C/pnetcdf_put_vara.c's pattern: a record
+ *       variable x(time, n) NC_INT, each record put once (appended), then
+ *       each record got once; per-call medians, loop and close times.
+ *   api_check c1ab <nc> <n> <nrec> <knob> <a> <b>
+ *       c1first with a libpncx knob alternating between a and b record by
+ *       record: put and get medians under each value (A/B in one process).
  *   api_check numrecs <nc>
  *       on N ranks: collective record puts must leave numrecs in the FILE
  *       (ncmpio_getput.m4:272-311), fixed-size puts must not touch it; rank
@@ -347,6 +354,150 @@ static void phases_print(const char *label, int calls)
         printf("%s\"%s\": [%.2f, %.2f]", k++ ? ", " : "", name(id), us / calls, (double)n / calls);
     }
     printf("}");
+}
+
+/* config 1 under the reference's own access pattern (benchmarks/C/
+ * pnetcdf_put_vara.c:193-209): a record variable x(time, n) NC_INT, each
+ * record put exactly once with ncmpi_put_vara_int_all (appended past the
+ * end of the file, numrecs written by the collective put), then each record
+ * got once with ncmpi_get_vara_int_all; per-call medians, plus the put loop,
+ * the get loop and the close timed whole.  Every record's values differ
+ * (record r holds v + r), and every element read back is checked. */
+static int mode_c1first(const char *path, MPI_Offset n, int nrec, int dev)
+{
+    int *h = (int *)malloc((size_t)n * 4), *g = (int *)calloc((size_t)n, 4), ncid, dimid[2], varid, r, bad = 0;
+    double *tp = (double *)calloc((size_t)nrec, sizeof(double)), *tg = (double *)calloc((size_t)nrec, sizeof(double));
+    double put_loop, get_loop, t_close, t0;
+    void *dh = NULL, *dg = NULL;
+    MPI_Offset start[2] = {0, 0}, count[2] = {1, n}, off = 0, i, nr = 0;
+    double put_us[64] = {0};
+    long long put_n[64] = {0};
+    for (i = 0; i < n; i++) h[i] = (int)((uint32_t)i * 2654435761u);
+    if (dev) {
+        dh = to_dev(NULL, (size_t)n * 4);
+        dg = to_dev(NULL, (size_t)n * 4);
+    }
+    CHECK(ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid));
+    CHECK(ncmpi_def_dim(ncid, "time", NC_UNLIMITED, &dimid[0]));
+    CHECK(ncmpi_def_dim(ncid, "x", n, &dimid[1]));
+    CHECK(ncmpi_def_var(ncid, "v", NC_INT, 2, dimid, &varid));
+    CHECK(ncmpi_enddef(ncid));
+    CHECK(ncmpi_inq_varoffset(ncid, varid, &off));
+    if (phases_on()) phases_reset();
+    put_loop = MPI_Wtime();
+    for (r = 0; r < nrec; r++) {
+        for (i = 0; i < n; i++) h[i] += 1;                   /* a new record's values */
+        if (dev && hipMemcpy(dh, h, (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess) { fprintf(stderr, "H2D failed\n"); exit(3); }
+        start[0] = r;
+        if (r == 1 && phases_on()) phases_reset();           /* phases of the calls after the first */
+        t0 = MPI_Wtime();
+        CHECK(ncmpi_put_vara_int_all(ncid, varid, start, count, dev ? dh : (void *)h));
+        tp[r] = MPI_Wtime() - t0;
+    }
+    put_loop = MPI_Wtime() - put_loop;
+    if (phases_on()) {                  /* keep the put sums for printing after the get loop */
+        const char *(*name)(int) = (const char *(*)(int))dlsym(RTLD_DEFAULT, "pncx_phase_name");
+        int (*rd)(int, double *, long long *) = (int (*)(int, double *, long long *))dlsym(RTLD_DEFAULT, "pncx_phase_read");
+        int id;
+        for (id = 0; name && rd && name(id) != NULL && id < 64; id++) rd(id, &put_us[id], &put_n[id]);
+        phases_reset();
+    }
+    CHECK(ncmpi_inq_dimlen(ncid, dimid[0], &nr));
+    if (nr != nrec) { fprintf(stderr, "c1first: numrecs %lld != %d\n", (long long)nr, nrec); nerrs++; }
+    for (i = 0; i < n; i++) h[i] -= nrec;                    /* record 0's values */
+    get_loop = 0;
+    for (r = 0; r < nrec; r++) {
+        start[0] = r;
+        if (r == 1 && phases_on()) phases_reset();
+        t0 = MPI_Wtime();
+        CHECK(ncmpi_get_vara_int_all(ncid, varid, start, count, dev ? dg : (void *)g));
+        tg[r] = MPI_Wtime() - t0;
+        get_loop += tg[r];
+        if (dev) from_dev(g, dg, (size_t)n * 4);
+        for (i = 0; i < n && !bad; i++) bad = g[i] != h[i] + r + 1;
+    }
+    t0 = MPI_Wtime();
+    CHECK(ncmpi_close(ncid));
+    t_close = MPI_Wtime() - t0;
+    if (bad) { fprintf(stderr, "c1first: get differs from put\n"); nerrs++; }
+    qsort(tp, (size_t)nrec, sizeof(double), cmp_dbl);
+    qsort(tg, (size_t)nrec, sizeof(double), cmp_dbl);
+    printf("{\"mode\": \"c1first\", \"n\": %lld, \"nrec\": %d, \"dev\": %d, \"rec_offset\": %lld, "
+           "\"put_ms_median\": %.5f, \"put_ms_min\": %.5f, \"get_ms_median\": %.5f, \"get_ms_min\": %.5f, "
+           "\"put_loop_ms\": %.4f, \"get_loop_ms\": %.4f, \"close_ms\": %.4f, \"errors\": %d",
+           (long long)n, nrec, dev, (long long)off, 1e3 * tp[nrec / 2], 1e3 * tp[0], 1e3 * tg[nrec / 2], 1e3 * tg[0],
+           1e3 * put_loop, 1e3 * get_loop, 1e3 * t_close, nerrs);
+    if (phases_on()) {
+        const char *(*name)(int) = (const char *(*)(int))dlsym(RTLD_DEFAULT, "pncx_phase_name");
+        int id, k = 0;
+        printf(", \"put_phases\": {");
+        for (id = 0; name && name(id) != NULL && id < 64; id++)
+            if (put_n[id] > 0)
+                printf("%s\"%s\": [%.2f, %.2f]", k++ ? ", " : "", name(id), put_us[id] / (nrec - 1),
+                       (double)put_n[id] / (nrec - 1));
+        printf("}");
+        phases_print("get_phases", nrec - 1);
+    }
+    printf("}\n");
+    if (dev) { hipFree(dh); hipFree(dg); }
+    free(h); free(g); free(tp); free(tg);
+    return nerrs != 0;
+}
+
+/* c1first with a libpncx knob alternating between two values record by
+ * record (A/B in one process, so both settings see the same box state):
+ * medians of the puts and gets under each value */
+static int mode_c1ab(const char *path, MPI_Offset n, int nrec, const char *knob, long long va, long long vb)
+{
+    int *h = (int *)malloc((size_t)n * 4), *g = (int *)calloc((size_t)n, 4), ncid, dimid[2], varid, r, bad = 0;
+    double *tp[2], *tg[2], t0;
+    int np[2] = {0, 0}, ng[2] = {0, 0}, k;
+    int (*kset)(const char *, long long) = (int (*)(const char *, long long))dlsym(RTLD_DEFAULT, "pncx_knob_set");
+    MPI_Offset start[2] = {0, 0}, count[2] = {1, n}, i;
+    for (k = 0; k < 2; k++) {
+        tp[k] = (double *)calloc((size_t)nrec, sizeof(double));
+        tg[k] = (double *)calloc((size_t)nrec, sizeof(double));
+    }
+    if (kset == NULL) { fprintf(stderr, "no pncx_knob_set\n"); return 1; }
+    for (i = 0; i < n; i++) h[i] = (int)((uint32_t)i * 2654435761u);
+    CHECK(ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid));
+    CHECK(ncmpi_def_dim(ncid, "time", NC_UNLIMITED, &dimid[0]));
+    CHECK(ncmpi_def_dim(ncid, "x", n, &dimid[1]));
+    CHECK(ncmpi_def_var(ncid, "v", NC_INT, 2, dimid, &varid));
+    CHECK(ncmpi_enddef(ncid));
+    for (r = 0; r < nrec; r++) {
+        k = (r / 2) % 2 ^ (r % 2);                      /* A B B A A B B A ...: no order bias */
+        for (i = 0; i < n; i++) h[i] += 1;
+        start[0] = r;
+        kset(knob, k ? vb : va);
+        t0 = MPI_Wtime();
+        CHECK(ncmpi_put_vara_int_all(ncid, varid, start, count, h));
+        if (r > 0) tp[k][np[k]++] = MPI_Wtime() - t0;
+    }
+    for (i = 0; i < n; i++) h[i] -= nrec;
+    for (r = 0; r < nrec; r++) {
+        k = (r / 2) % 2 ^ (r % 2);
+        start[0] = r;
+        kset(knob, k ? vb : va);
+        t0 = MPI_Wtime();
+        CHECK(ncmpi_get_vara_int_all(ncid, varid, start, count, g));
+        if (r > 0) tg[k][ng[k]++] = MPI_Wtime() - t0;
+        for (i = 0; i < n && !bad; i++) bad = g[i] != h[i] + r + 1;
+    }
+    kset(knob, -1);
+    CHECK(ncmpi_close(ncid));
+    if (bad) { fprintf(stderr, "c1ab: get differs from put\n"); nerrs++; }
+    printf("{\"mode\": \"c1ab\", \"knob\": \"%s\"", knob);
+    for (k = 0; k < 2; k++) {
+        qsort(tp[k], (size_t)np[k], sizeof(double), cmp_dbl);
+        qsort(tg[k], (size_t)ng[k], sizeof(double), cmp_dbl);
+        printf(", \"%lld\": {\"put_ms\": %.4f, \"get_ms\": %.4f}", k ? vb : va, 1e3 * tp[k][np[k] / 2],
+               1e3 * tg[k][ng[k] / 2]);
+        free(tp[k]); free(tg[k]);
+    }
+    printf(", \"errors\": %d}\n", nerrs);
+    free(h); free(g);
+    return nerrs != 0;
 }
 
 /* config 1 timed (bench.py's c1 leg): one open file, reps puts then reps gets.
@@ -716,6 +867,10 @@ int main(int argc, char **argv)
         rc = mode_c1(argv[2], argv[3], atoll(argv[4]), argc >= 6 ? atoi(argv[5]) : 0);
     else if (argc >= 6 && strcmp(argv[1], "c1bench") == 0)
         rc = mode_c1bench(argv[2], atoll(argv[3]), atoi(argv[4]), atoi(argv[5]));
+    else if (argc >= 6 && strcmp(argv[1], "c1first") == 0)
+        rc = mode_c1first(argv[2], atoll(argv[3]), atoi(argv[4]), atoi(argv[5]));
+    else if (argc >= 8 && strcmp(argv[1], "c1ab") == 0)
+        rc = mode_c1ab(argv[2], atoll(argv[3]), atoi(argv[4]), argv[5], atoll(argv[6]), atoll(argv[7]));
     else if (argc >= 3 && strcmp(argv[1], "numrecs") == 0) rc = mode_numrecs(argv[2]);
     else if (argc >= 3 && strcmp(argv[1], "openfail") == 0) rc = mode_openfail(argv[2]);
     else if (argc >= 3 && strcmp(argv[1], "bputshort") == 0) rc = mode_bputshort(argv[2]);

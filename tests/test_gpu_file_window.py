@@ -196,3 +196,96 @@ def test_window_churn_guard(gpu, shm_dir, knob):
     h = cdfparse.parse_cdf(raw)
     v = h["vars"][0]
     assert np.array_equal(np.frombuffer(raw[v["begin"]:v["begin"] + 4 * 11 * n], ">i4"), ref[:11 * n])
+
+
+def test_window_tail_record_past_eof(gpu, shm_dir, knob):
+    """A window's last page runs past the end of the file.  A record smaller
+    than a page appended after the window was made lands in that page: the
+    file must grow to the record's end (what pwrite does), pread and a
+    reopen must see the record, and the bytes must be the oracle's
+    (a write hit past i_size left the bytes invisible)."""
+    from pnetcdf_amd import pncx
+    knob("FILE_WINDOW", 2)                         # a window at first use
+    n, m = 3 * (1 << 16) + 5, 100                  # the fixed variable ends mid-page
+    p = os.path.join(shm_dir, "tail.nc")
+    err, ncid = N.create(p, N.NC_64BIT_DATA)
+    N.def_dim(ncid, "t", N.NC_UNLIMITED)
+    N.def_dim(ncid, "x", n)
+    N.def_dim(ncid, "y", m)
+    N.def_var(ncid, "fix", T.NC_INT, [1])
+    N.def_var(ncid, "rec", T.NC_INT, [0, 2])
+    assert N.enddef(ncid) == 0
+    a = np.arange(n, dtype=np.int32) * 3 - 7
+    pncx.phases(1)
+    assert N.put_var(ncid, 0, a) == 0              # makes the window over the file's end
+    recs = [np.arange(m, dtype=np.int32) + 1000 * (r + 1) for r in range(2)]
+    for r, b in enumerate(recs):
+        assert N.put_var(ncid, 1, b, [r, 0], [1, m]) == 0
+    uses = pncx.phase_sums().get("file.window_use", (0, 0))[1]
+    pncx.phases(0)
+    assert uses >= 2, "the record puts did not go through the window"
+    h = cdfparse.parse_cdf(open(p, "rb").read())
+    rv = [v for v in h["vars"] if v["name"] == "rec"][0]
+    end = rv["begin"] + 2 * 4 * m
+    assert os.path.getsize(p) >= end, "the window stored bytes past the end of the file"
+    with open(p, "rb") as fh:                      # pread, not the mapping
+        fh.seek(rv["begin"])
+        raw = fh.read(2 * 4 * m)
+    assert raw == b"".join(r.astype(">i4").tobytes() for r in recs)
+    o = np.zeros(m, np.int32)
+    assert N.get_var(ncid, 1, o, [1, 0], [1, m]) == 0 and np.array_equal(o, recs[1])
+    assert N.close(ncid) == 0
+    err, ncid = N.open(p)
+    assert err == 0
+    for r, b in enumerate(recs):
+        o = np.zeros(m, np.int32)
+        assert N.get_var(ncid, 1, o, [r, 0], [1, m]) == 0 and np.array_equal(o, b)
+    assert N.close(ncid) == 0
+
+
+def test_window_device_buffer_follows_user_stream(gpu, shm_dir, knob):
+    """Device-buffer calls through a window run on the library's stream; they
+    must still follow the caller's stream: a put of a buffer a kernel on the
+    caller's stream is still producing, and a get into a buffer an earlier
+    kernel on that stream still reads."""
+    torch = gpu
+    from pnetcdf_amd import pncx
+    knob("FILE_WINDOW", 2)
+    n = 1 << 20
+    p = os.path.join(shm_dir, "stream.nc")
+    err, ncid = N.create(p, N.NC_64BIT_DATA)
+    N.def_dim(ncid, "x", n)
+    N.def_var(ncid, "v", T.NC_INT, [0])
+    assert N.enddef(ncid) == 0
+    s = torch.cuda.Stream()
+    want = torch.arange(n, dtype=torch.int32, device="cuda") * 5 + 1
+    old = torch.full((n,), -3, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    pncx.phases(1)
+    for rep in range(3):
+        t = old.clone()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(20_000_000)          # the producer is late
+            t.copy_(want + rep)
+        assert N.put_var_dev(ncid, 0, t, stream=s) == 0
+        s.synchronize()
+        raw = open(p, "rb").read()
+        h = cdfparse.parse_cdf(raw)
+        v = h["vars"][0]
+        got = np.frombuffer(raw[v["begin"]:v["begin"] + 4 * n], ">i4")
+        assert np.array_equal(got, (want + rep).cpu().numpy()), f"put read the buffer early (rep {rep})"
+    for rep in range(2):
+        t = old.clone()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(20_000_000)
+            seen = t.clone()                       # an earlier reader of t on the caller's stream
+        assert N.get_var_dev(ncid, 0, t, stream=s) == 0
+        s.synchronize()
+        assert bool((seen == -3).all()), "the get overwrote the buffer before an earlier reader ran"
+        assert torch.equal(t, want + 2)
+    uses = pncx.phase_sums().get("file.window_use", (0, 0))[1]
+    pncx.phases(0)
+    assert uses >= 4, "the calls did not take the window"
+    assert N.close(ncid) == 0
