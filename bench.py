@@ -299,6 +299,17 @@ def load_traffic(kernel_key, elems_per_launch):
         return None
 
 
+def traffic_source():
+    """Which PMC pass roofline.traffic comes from: the summary file and the
+    round tag tools/pmc_summary.py wrote into it."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(p))
+        return {"file": "profiles/pmc_traffic.json", "round": d.get("round"), "pmc_csv": d.get("source")}
+    except Exception:
+        return None
+
+
 # --------------------------------------------------------------- workloads
 class Workload:
     """One single-GPU configuration: buffers in HBM, a launch() = one step,
@@ -555,6 +566,7 @@ def summary(wl, elapsed, kern_ms, call_ms, steps, world):
     achieved = wl.bytes_per_elem * wl.elems / (kern_ms * 1e-3) / 1e9         # GB/s per GPU, per launch
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(wl.metric_key, wl.elems),
+            "traffic_source": traffic_source(),
             "kernel": wl.kernel, "kernel_ms_avg": round(kern_ms, 4),
             "algorithmic_bytes_per_launch": int(wl.bytes_per_elem * wl.elems)}
     if call_ms is not None:

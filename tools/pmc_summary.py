@@ -85,6 +85,7 @@ def main():
                        "WRITE_SIZE as is; both KiB; summed over a step's product kernels); "
                        "written by tools/pmc_summary.py")
     old["round"] = tag
+    old["source"] = f"profiles/{tag}_pmc.csv"
     json.dump(old, open(p, "w"), indent=1)
     print(json.dumps(kernels, indent=1))
 
