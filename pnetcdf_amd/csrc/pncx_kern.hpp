@@ -1209,7 +1209,8 @@ struct TransposeGeom {
     int64_t tp, tu;          // tiles along P and U
     int64_t ntiles;          // tp * tu * outer
     int     nod;             // outer dims
-    int     diag;            // skewed tile order: tile (tp, tu) runs as ((tp + diag * tu) % tp_count, tu); 0 row-major
+    int     diag;            // skewed tile order: tile (tp, tu) runs as ((tp + diag * tu) % tp_count, tu); 0 row-major;
+                             // < 0: (tp + hash(tu)) % tp_count
     int64_t ocount[PNCX_MAX_DIMS], ostride_p[PNCX_MAX_DIMS], ostride_u[PNCX_MAX_DIMS];
 };
 
@@ -1409,9 +1410,14 @@ __global__ __launch_bounds__(256, 2) void k_imap_tile(const uint8_t *src, uint8_
         // share p0, so with a power-of-two leading dimension their packed-side
         // columns all sit at the same address bits below the 2^k stride.
         // Shifting p by u spreads them (a bijection on (tp, tu) for fixed tu).
-        if (g.diag) {
+        if (g.diag > 0) {
             tp += tu * g.diag;
             if (tp >= g.tp) tp %= g.tp;
+        } else if (g.diag < 0) {
+            // hashed: each u tile row starts at a pseudo-random p tile
+            // (multiplicative hash of tu), still a bijection for fixed tu
+            tp += (int64_t)(((uint32_t)tu * 0x9E3779B1u) >> 8) % g.tp;
+            if (tp >= g.tp) tp -= g.tp;
         }
         const int64_t p0 = tp * XT_P, u0 = tu * XT_U;
         const int np = (int)(g.cp - p0 < XT_P ? g.cp - p0 : XT_P), nu = (int)(g.cu - u0 < XT_U ? g.cu - u0 : XT_U);
@@ -1452,7 +1458,7 @@ __global__ __launch_bounds__(256, 2) void k_imap_tile(const uint8_t *src, uint8_
 
 int xpose_merge();   // PNCX_XPOSE_MERGE=0 tiles P alone (A/B); default 1
 int tgap_enabled();  // PNCX_TGAP=0: 8-bit gap maps (tmode 6) on k_imap
-int xpose_order();   // PNCX_XPOSE_ORDER: 0 row-major tiles, 1 diagonal, k >= 2 skew k, -1 (unset) by shape
+int xpose_order();   // PNCX_XPOSE_ORDER: 0 row-major tiles, 1 diagonal, k >= 2 skew k, 1000 hashed, -1 (unset) by shape
 
 // Pick the transpose kernel for a varm layout: P = last dim, U = the other
 // dim with the smallest imap; worth it when P is strided in the user buffer
@@ -1505,7 +1511,7 @@ inline bool transpose_geom(const pncxk_imap *m, TransposeGeom *g, bool merge) {
     // PNCX_XPOSE_ORDER=0 / 1 forces row-major / diagonal.
     {
         const int o = xpose_order();
-        g->diag = o < 0 ? !mrg : o;      // >= 2: skew of o tiles per u tile
+        g->diag = o < 0 ? !mrg : (o == 1000 ? -1 : o);   // >= 2: skew of o tiles per u tile; 1000: hashed
     }
     return g->ntiles > 0;
 }
