@@ -32,10 +32,11 @@ def exe(name):
     return p
 
 
-def run(args, nprocs=1, timeout=300, check=True):
-    """Run a tests/mpi program, under mpiexec when nprocs > 1."""
+def run(args, nprocs=1, timeout=300, check=True, env=None):
+    """Run a tests/mpi program, under mpiexec when nprocs > 1 (env: the
+    environment to use instead of this process's)."""
     cmd = ([MPIEXEC, "-n", str(nprocs)] if nprocs > 1 else []) + list(args)
-    env = dict(os.environ)
+    env = dict(os.environ if env is None else env)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=MPI_DIR)
     if check:
