@@ -315,15 +315,16 @@ def test_flex_short_runs_many_steps(torch_cuda, xt, it):
 
 
 @pytest.mark.parametrize("urun", ["1", "0"])
-@pytest.mark.parametrize("blen,gap", [(2, 2), (64, 16), (300, 4), (3, 1)])
+@pytest.mark.parametrize("blen,gap", [(2, 2), (64, 16), (300, 4), (3, 1), (1, 1), (5, 11)])
 @pytest.mark.parametrize("xt,it", [(T.NC_DOUBLE, T.ITYPE_DOUBLE), (T.NC_FLOAT, T.ITYPE_DOUBLE),
                                    (T.NC_SHORT, T.ITYPE_INT), (T.NC_INT, T.ITYPE_SHORT)])
 @pytest.mark.parametrize("where", ["host", "dev"])
 def test_flex_uniform_vector_runs(torch_cuda, where, xt, it, blen, gap, urun, knob):
     """uniform runs whose lengths hold whole 16-byte vectors, 16-byte aligned,
     over a contiguous count: one vector per lane (k_urun; PNCX_URUN=0 takes
-    k_imap / k_tmap_runs).  blen 3 does not divide into vectors and falls
-    back either way.  3 copies, NC_ERANGE from int -> NC_SHORT."""
+    k_imap / k_tmap_runs).  Blocks that do not divide into vectors (1, 3, 5;
+    2 of NC_FLOAT <- double) fall back to k_imap either way.  3 copies,
+    NC_ERANGE from int -> NC_SHORT."""
     knob("URUN", urun)
     nb = 4096 if blen <= 64 else 64
     disp = (np.arange(nb) * (blen + gap)).tolist()
