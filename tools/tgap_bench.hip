@@ -471,18 +471,27 @@ float run_lds(const uint8_t *s, uint8_t *d, uint32_t nunits, uint32_t nq, uint32
     return ms / 20;
 }
 
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
+    const uint32_t per = nb / 8, rem = nb % 8, x = b % 8, k = b / 8;
+    return (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + k;
+}
+
 // store policy on the packed side: 0 nt (as k_gather), 1 plain write-back,
-// 2 nt sc1 (st_stream in the library), with nontemporal user-side loads
+// 2 nt sc1 (st_stream in the library), with nontemporal user-side loads;
+// round 5: 3 / 4 = the lanes whose 128-byte line the chunk covers only in
+// part store write-back (the neighbouring chunk, usually a wave of the same
+// block, fills the rest in L2 before it goes out whole), the others nt / nt sc1.
+// Blocks in XCD order as k_tgap.
 template <int U, int SP>
 __global__ __launch_bounds__(256) void k_gather_sp(const uint8_t *src, uint8_t *dst, uint32_t nunits, uint32_t nq,
                                                    uint32_t tn, int64_t textent, const unsigned *toff,
                                                    const unsigned char *nib) {
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t step = gridDim.x * 4 * U;
-    for (uint32_t u0 = blockIdx.x * 4 * U; u0 < nunits; u0 += step) {
+    for (uint32_t u0 = xcd_remap(blockIdx.x, gridDim.x) * 4 * U; u0 < nunits; u0 += step) {
         uint64_t sv[U];
         int64_t ko[U];
-        bool ok[U];
+        bool ok[U], edge[U];
 #pragma unroll
         for (int i = 0; i < U; i++) {
             uint32_t u = u0 + i * 4 + w;
@@ -491,6 +500,9 @@ __global__ __launch_bounds__(256) void k_gather_sp(const uint8_t *src, uint8_t *
             const uint32_t c = u / nq, q = u - c * nq, r = q * 64 + lane, rc = r < tn ? r : tn - 1;
             ok[i] = okw && r < tn;
             ko[i] = (int64_t)c * tn + rc;
+            const int64_t lo = ((int64_t)c * tn + q * 64) * 8, hi = lo + (int64_t)(tn - q * 64 < 64 ? tn - q * 64 : 64) * 8;
+            const int64_t line = (ko[i] * 8) & ~(int64_t)127;
+            edge[i] = line < lo || line + 128 > hi;
             const uint32_t b = nib[(int64_t)q * 32 + (lane >> 1)];
             const uint32_t g = wave_inclusive_sum((b >> ((lane & 1) * 4)) & 15u);
             const uint8_t *p = src + (int64_t)c * textent + toff[q] + (int64_t)((rc & 63) + g) * 8;
@@ -503,6 +515,9 @@ __global__ __launch_bounds__(256) void k_gather_sp(const uint8_t *src, uint8_t *
                 const uint64_t v = __builtin_bswap64(sv[i]);
                 if constexpr (SP == 0) __builtin_nontemporal_store(v, p);
                 else if constexpr (SP == 1) *p = v;
+                else if constexpr (SP == 2) asm volatile("global_store_dwordx2 %0, %1, off nt sc1" ::"v"(p), "v"(v) : "memory");
+                else if (edge[i]) *p = v;
+                else if constexpr (SP == 3) __builtin_nontemporal_store(v, p);
                 else asm volatile("global_store_dwordx2 %0, %1, off nt sc1" ::"v"(p), "v"(v) : "memory");
             }
     }
@@ -614,11 +629,28 @@ int main() {
                    alg / run_sc<2, 2>(pk, u1, nunits, nq, tn, ext, t, nbp) / 1e6);
         hipFree(pk); hipFree(u1); hipFree(u2);
     }
-    for (int rep = 0; rep < 2; rep++)
-        printf("tn %u (tn %% 64 = %u): store nt %.1f  write-back %.1f  nt sc1 %.1f | U2: nt %.1f  wb %.1f GB/s\n", tn, tn % 64,
+    {
+        // edge-line store variants write the same packed bytes as nt
+        std::vector<uint8_t> h1((size_t)tn * copies * 8), h2(h1.size());
+        hipMemset(d, 0, h1.size());
+        run_sp<4, 0>(s, d, nunits, nq, tn, ext, t, nbp);
+        hipMemcpy(h1.data(), d, h1.size(), hipMemcpyDeviceToHost);
+        for (int m = 3; m <= 4; m++) {
+            hipMemset(d, 0, h1.size());
+            if (m == 3) run_sp<4, 3>(s, d, nunits, nq, tn, ext, t, nbp);
+            else run_sp<4, 4>(s, d, nunits, nq, tn, ext, t, nbp);
+            hipMemcpy(h2.data(), d, h2.size(), hipMemcpyDeviceToHost);
+            printf("edge-line store variant %d %s nt\n", m, h1 == h2 ? "matches" : "DIFFERS from");
+        }
+    }
+    for (int rep = 0; rep < 3; rep++)
+        printf("tn %u (tn %% 64 = %u): store nt %.1f  write-back %.1f  nt sc1 %.1f  edge-wb+nt %.1f  edge-wb+nt-sc1 %.1f"
+               " | U2: nt %.1f  wb %.1f GB/s\n", tn, tn % 64,
                alg / run_sp<4, 0>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
                alg / run_sp<4, 1>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
                alg / run_sp<4, 2>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
+               alg / run_sp<4, 3>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
+               alg / run_sp<4, 4>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
                alg / run_sp<2, 0>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6,
                alg / run_sp<2, 1>(s, d, nunits, nq, tn, ext, t, nbp) / 1e6);
     for (int rep = 0; rep < 0; rep++)
