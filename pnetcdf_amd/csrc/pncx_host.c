@@ -100,13 +100,13 @@ static const char *const g_ph_names[PH_N] = {
     "put.plan", "put.register", "put.convert", "put.write", "put.wait", "put.unregister", "put.total",
     "get.plan", "get.register", "get.read", "get.convert", "get.unregister", "get.total",
     "conv.lock_pin", "conv.enqueue", "conv.sync", "conv.status", "conv.unpin",
-    "gpu.h2d", "gpu.kernel", "gpu.d2h", "file.window_map", "file.window_use", "put.grow"};
+    "gpu.h2d", "gpu.kernel", "gpu.d2h", "file.window_map", "file.window_use", "put.grow", "warm"};
 
 /* A/B knobs (pncx_shim.h): the environment once at load, then pncx_knob_set */
 static const char *const g_knob_names[PNCXK_NKNOB] = {
     "TILE_U", "XPOSE_MERGE", "URUN", "TMAP_VEC", "IMAP_ROWS", "FUSE_LANES", "BATCH_FUSE", "TMAP_IMAP",
     "TOFF16", "TOFF_MAX_ELEMS", "XPOSE_ORDER", "TOFF_RUNS", "HOST_ZC", "IO_INLINE_MB", "FILE_WINDOW", "IO_POPULATE", "HOST_ZC_MAX_MB", "TGAP",
-    "GROW", "READ_SPLIT"};
+    "GROW", "READ_SPLIT", "WARM"};
 static long long g_knob[PNCXK_NKNOB];
 
 long long pncx_knob(int id)
@@ -643,6 +643,22 @@ static int stage_slots(ctx_t *c, size_t slot_bytes)
         if (pncxrt_malloc(&c->sdbuf[i], slot_bytes) != 0) return PNCX_EDEVICE;
     c->sdbuf_size = slot_bytes;
     return 0;
+}
+
+/* What the first staged call on this device would set up: the context
+ * (streams, status words), the chunk events, the pinned status word, and
+ * every kernel file's code object.  The file layer runs it on a thread at
+ * create/open (pncx_nc.c, warm_start). */
+int pncx_warmup(void)
+{
+    ctx_t *c;
+    int err;
+    if (!have_device() || (c = get_ctx()) == NULL) return PNCX_EDEVICE;
+    pthread_mutex_lock(&c->lock);
+    err = stage_slots(c, 0);
+    pthread_mutex_unlock(&c->lock);
+    if (!err && pncxrt_load_code_objects() != 0) err = PNCX_EDEVICE;
+    return err;
 }
 
 /* elements per chunk for a call of n elements: about 4 chunks, each of

@@ -35,6 +35,7 @@ enum {
     PH_WIN_MAP,         /* a file window mapped and registered             */
     PH_WIN_USE,         /* a request converted through a file window       */
     PH_PUT_GROW,        /* appended pages allocated while the GPU converts */
+    PH_WARM,            /* the create/open warm-up thread, start to end    */
     PH_N
 };
 

@@ -184,6 +184,7 @@ enum {
     PNCXK_KNOB_GROW,            /* 0: no fallocate of appended ranges while
                                  * the GPU converts (tmpfs)                  */
     PNCXK_KNOB_READ_SPLIT,      /* pool preads per chunk of an inline get    */
+    PNCXK_KNOB_WARM,            /* 0: no device/staging warm-up at create/open */
     PNCXK_NKNOB
 };
 long long pncx_knob(int id);
@@ -192,6 +193,7 @@ long long pncx_knob(int id);
 int  pncxrt_device_count(void);
 int  pncxrt_set_device(int dev);
 int  pncxrt_get_device(void);
+int  pncxrt_load_code_objects(void);   /* every kernel file's code object on the current device */
 int  pncxrt_malloc(void **p, size_t n);
 int  pncxrt_free(void *p);
 int  pncxrt_host_alloc(void **p, size_t n);

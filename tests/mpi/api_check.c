@@ -367,21 +367,24 @@ static int mode_c1first(const char *path, MPI_Offset n, int nrec, int dev)
 {
     int *h = (int *)malloc((size_t)n * 4), *g = (int *)calloc((size_t)n, 4), ncid, dimid[2], varid, r, bad = 0;
     double *tp = (double *)calloc((size_t)nrec, sizeof(double)), *tg = (double *)calloc((size_t)nrec, sizeof(double));
-    double put_loop, get_loop, t_close, t0;
+    double put_loop, get_loop, t_close, t0, t_open, t_create;
     void *dh = NULL, *dg = NULL;
     MPI_Offset start[2] = {0, 0}, count[2] = {1, n}, off = 0, i, nr = 0;
-    double put_us[64] = {0};
-    long long put_n[64] = {0};
+    double put_us[64] = {0}, first_us[64] = {0}, put_first = 0, get_first = 0;
+    long long put_n[64] = {0}, first_n[64] = {0};
     for (i = 0; i < n; i++) h[i] = (int)((uint32_t)i * 2654435761u);
     if (dev) {
         dh = to_dev(NULL, (size_t)n * 4);
         dg = to_dev(NULL, (size_t)n * 4);
     }
+    t_open = MPI_Wtime();
     CHECK(ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid));
+    t_create = MPI_Wtime() - t_open;
     CHECK(ncmpi_def_dim(ncid, "time", NC_UNLIMITED, &dimid[0]));
     CHECK(ncmpi_def_dim(ncid, "x", n, &dimid[1]));
     CHECK(ncmpi_def_var(ncid, "v", NC_INT, 2, dimid, &varid));
     CHECK(ncmpi_enddef(ncid));
+    t_open = MPI_Wtime() - t_open;                           /* create through enddef */
     CHECK(ncmpi_inq_varoffset(ncid, varid, &off));
     if (phases_on()) phases_reset();
     put_loop = MPI_Wtime();
@@ -389,12 +392,19 @@ static int mode_c1first(const char *path, MPI_Offset n, int nrec, int dev)
         for (i = 0; i < n; i++) h[i] += 1;                   /* a new record's values */
         if (dev && hipMemcpy(dh, h, (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess) { fprintf(stderr, "H2D failed\n"); exit(3); }
         start[0] = r;
-        if (r == 1 && phases_on()) phases_reset();           /* phases of the calls after the first */
+        if (r == 1 && phases_on()) {                         /* phases of the calls after the first */
+            const char *(*name)(int) = (const char *(*)(int))dlsym(RTLD_DEFAULT, "pncx_phase_name");
+            int (*rd)(int, double *, long long *) = (int (*)(int, double *, long long *))dlsym(RTLD_DEFAULT, "pncx_phase_read");
+            int id;
+            for (id = 0; name && rd && name(id) != NULL && id < 64; id++) rd(id, &first_us[id], &first_n[id]);
+            phases_reset();
+        }
         t0 = MPI_Wtime();
         CHECK(ncmpi_put_vara_int_all(ncid, varid, start, count, dev ? dh : (void *)h));
         tp[r] = MPI_Wtime() - t0;
     }
     put_loop = MPI_Wtime() - put_loop;
+    put_first = tp[0];
     if (phases_on()) {                  /* keep the put sums for printing after the get loop */
         const char *(*name)(int) = (const char *(*)(int))dlsym(RTLD_DEFAULT, "pncx_phase_name");
         int (*rd)(int, double *, long long *) = (int (*)(int, double *, long long *))dlsym(RTLD_DEFAULT, "pncx_phase_read");
@@ -413,6 +423,7 @@ static int mode_c1first(const char *path, MPI_Offset n, int nrec, int dev)
         CHECK(ncmpi_get_vara_int_all(ncid, varid, start, count, dev ? dg : (void *)g));
         tg[r] = MPI_Wtime() - t0;
         get_loop += tg[r];
+        if (r == 0) get_first = tg[0];
         if (dev) from_dev(g, dg, (size_t)n * 4);
         for (i = 0; i < n && !bad; i++) bad = g[i] != h[i] + r + 1;
     }
@@ -424,12 +435,20 @@ static int mode_c1first(const char *path, MPI_Offset n, int nrec, int dev)
     qsort(tg, (size_t)nrec, sizeof(double), cmp_dbl);
     printf("{\"mode\": \"c1first\", \"n\": %lld, \"nrec\": %d, \"dev\": %d, \"rec_offset\": %lld, "
            "\"put_ms_median\": %.5f, \"put_ms_min\": %.5f, \"get_ms_median\": %.5f, \"get_ms_min\": %.5f, "
-           "\"put_loop_ms\": %.4f, \"get_loop_ms\": %.4f, \"close_ms\": %.4f, \"errors\": %d",
+           "\"put_loop_ms\": %.4f, \"get_loop_ms\": %.4f, \"close_ms\": %.4f, \"put_first_ms\": %.4f, "
+           "\"get_first_ms\": %.4f, \"create_ms\": %.4f, \"create_to_enddef_ms\": %.4f, \"errors\": %d",
            (long long)n, nrec, dev, (long long)off, 1e3 * tp[nrec / 2], 1e3 * tp[0], 1e3 * tg[nrec / 2], 1e3 * tg[0],
-           1e3 * put_loop, 1e3 * get_loop, 1e3 * t_close, nerrs);
+           1e3 * put_loop, 1e3 * get_loop, 1e3 * t_close, 1e3 * put_first, 1e3 * get_first, 1e3 * t_create,
+           1e3 * t_open, nerrs);
     if (phases_on()) {
         const char *(*name)(int) = (const char *(*)(int))dlsym(RTLD_DEFAULT, "pncx_phase_name");
         int id, k = 0;
+        printf(", \"first_put_phases\": {");
+        for (id = 0; name && name(id) != NULL && id < 64; id++)
+            if (first_n[id] > 0)
+                printf("%s\"%s\": [%.2f, %.2f]", k++ ? ", " : "", name(id), first_us[id], (double)first_n[id]);
+        printf("}");
+        k = 0;
         printf(", \"put_phases\": {");
         for (id = 0; name && name(id) != NULL && id < 64; id++)
             if (put_n[id] > 0)
