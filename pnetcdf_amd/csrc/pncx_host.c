@@ -646,9 +646,11 @@ static int stage_slots(ctx_t *c, size_t slot_bytes)
 }
 
 /* What the first staged call on this device would set up: the context
- * (streams, status words), the chunk events, the pinned status word, and
- * every kernel file's code object.  The file layer runs it on a thread at
- * create/open (pncx_nc.c, warm_start). */
+ * (streams, status words), the chunk events and the pinned status word.
+ * The file layer runs it on a thread at create/open (pncx_nc.c,
+ * warm_start).  Kernel code objects stay lazy: querying one attribute per
+ * kernel file to load them all made create..enddef 330-530 ms against the
+ * 4-6 ms one file costs at its first launch (profiles/r05l_first_call.txt). */
 int pncx_warmup(void)
 {
     ctx_t *c;
@@ -657,7 +659,6 @@ int pncx_warmup(void)
     pthread_mutex_lock(&c->lock);
     err = stage_slots(c, 0);
     pthread_mutex_unlock(&c->lock);
-    if (!err && pncxrt_load_code_objects() != 0) err = PNCX_EDEVICE;
     return err;
 }
 

@@ -128,11 +128,3 @@ extern "C" int pncxk_first_diff(const void *a, const void *b, long long n, int i
         default: return NC_EBADTYPE;
     }
 }
-
-// loads this file's gfx950 code object on the current device ahead of the
-// first launch (pncxrt_load_code_objects, pncx_kern_swap.hip)
-__global__ void k_load_diff() {}
-extern "C" int pncxk_load_diff(void) {
-    hipFuncAttributes fa;
-    return hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&k_load_diff)) == hipSuccess ? 0 : -1;
-}

@@ -82,11 +82,3 @@ extern "C" int pncxk_opinfo_get_get(int xtype, int itype, pncxk_opinfo *o) {
         default: return NC_EBADTYPE;
     }
 }
-
-// loads this file's gfx950 code object on the current device ahead of the
-// first launch (pncxrt_load_code_objects, pncx_kern_swap.hip)
-__global__ void k_load_get() {}
-extern "C" int pncxk_load_get(void) {
-    hipFuncAttributes fa;
-    return hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&k_load_get)) == hipSuccess ? 0 : -1;
-}

@@ -106,11 +106,3 @@ extern "C" int pncxk_opinfo_getput(int kind, int xtype, int itype, int preserve,
         default: return NC_EBADTYPE;
     }
 }
-
-// loads this file's gfx950 code object on the current device ahead of the
-// first launch (pncxrt_load_code_objects, pncx_kern_swap.hip)
-__global__ void k_load_put() {}
-extern "C" int pncxk_load_put(void) {
-    hipFuncAttributes fa;
-    return hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&k_load_put)) == hipSuccess ? 0 : -1;
-}

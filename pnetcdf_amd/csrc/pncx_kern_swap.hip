@@ -502,22 +502,6 @@ int pncxrt_device_count(void) {
     return n;
 }
 int pncxrt_set_device(int dev) { return rt(hipSetDevice(dev), "hipSetDevice"); }
-// HIP loads a file's code object on a device at the first launch of one of
-// its kernels (4-6 ms for the conversion files, profiles/r05k_first_call.txt);
-// a function-attribute query loads it too, so the file layer's warm-up
-// (pncx_warmup) can take that cost at create/open instead of the first put
-__global__ void k_load_swap() {}
-extern "C" int pncxk_load_put(void);
-extern "C" int pncxk_load_get(void);
-extern "C" int pncxk_load_diff(void);
-int pncxrt_load_code_objects(void) {
-    hipFuncAttributes fa;
-    int err = hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&k_load_swap)) == hipSuccess ? 0 : -1;
-    if (pncxk_load_put() != 0) err = -1;
-    if (pncxk_load_get() != 0) err = -1;
-    if (pncxk_load_diff() != 0) err = -1;
-    return err;
-}
 int pncxrt_get_device(void) {
     int d = -1;
     if (hipGetDevice(&d) != hipSuccess) return -1;
