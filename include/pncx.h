@@ -376,9 +376,10 @@ int  pncx_device_count(void);
 int  pncx_set_device(int dev);
 int  pncx_get_device(void);
 /* Set up ahead of the first data call on the current device what that call
- * would otherwise pay for: the device context (streams, status words) and
- * the staging events (no reference equivalent; ncmpi_create/ncmpi_open run
- * it on a thread, pncx_nc.c warm_start).  NC_NOERR or PNCX_EDEVICE. */
+ * would otherwise pay for: the device context (streams, status words), the
+ * staging events and the same-type swap kernels' code object (no reference
+ * equivalent; ncmpi_create/ncmpi_open run it on a thread, pncx_nc.c
+ * warm_start).  NC_NOERR or PNCX_EDEVICE. */
 int  pncx_warmup(void);
 /* Pin a long-lived host buffer for direct DMA (no reference equivalent: the
  * xbuf of ncmpio_getput.m4:216,422 is malloc'ed per call).  Host entry points

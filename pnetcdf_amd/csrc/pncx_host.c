@@ -646,11 +646,12 @@ static int stage_slots(ctx_t *c, size_t slot_bytes)
 }
 
 /* What the first staged call on this device would set up: the context
- * (streams, status words), the chunk events and the pinned status word.
- * The file layer runs it on a thread at create/open (pncx_nc.c,
- * warm_start).  Kernel code objects stay lazy: querying one attribute per
- * kernel file to load them all made create..enddef 330-530 ms against the
- * 4-6 ms one file costs at its first launch (profiles/r05l_first_call.txt). */
+ * (streams, status words), the chunk events, the pinned status word and the
+ * swap kernels' code object (4-5 ms).  The file layer runs it on a thread at
+ * create/open (pncx_nc.c, warm_start).  The per-type conversion objects stay
+ * lazy: loading every kernel file up front made create..enddef 330-530 ms
+ * (profiles/r05l_first_call_all_code_objects.txt), and a process converts
+ * few external types. */
 int pncx_warmup(void)
 {
     ctx_t *c;
@@ -659,6 +660,7 @@ int pncx_warmup(void)
     pthread_mutex_lock(&c->lock);
     err = stage_slots(c, 0);
     pthread_mutex_unlock(&c->lock);
+    if (!err && pncxrt_load_swap_code() != 0) err = PNCX_EDEVICE;
     return err;
 }
 

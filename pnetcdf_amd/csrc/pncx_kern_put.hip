@@ -5,6 +5,18 @@
 // already in xbuf.
 #include "pncx_pairs.hpp"
 
+// Compiled once per external type (-DPNCX_XT=<NC_* value>, Makefile): each
+// type's kernels are a code object of their own, which HIP loads on a device
+// at the first launch from it -- ~18 ms for one type's instead of 180 ms for
+// all ten (profiles/r05p_first_launch.txt).  pncx_kern_xt.c dispatches on
+// the external type.
+#ifndef PNCX_XT
+#error "compile with -DPNCX_XT=<external type>"
+#endif
+#define PNCX_FN2(name, x) name##_x##x
+#define PNCX_FN1(name, x) PNCX_FN2(name, x)
+#define PNCX_FN(name) PNCX_FN1(name, PNCX_XT)
+
 using namespace pncx;
 
 namespace {
@@ -43,29 +55,29 @@ int put_info(pncxk_opinfo *o) {
 
 #define PNCX_KEY(XT, IT) ((XT) * 16 + (IT))
 
-extern "C" int pncxk_put(int xtype, int itype, int preserve, const pncxk_args *a) {
+extern "C" int PNCX_FN(pncxk_put)(int xtype, int itype, int preserve, const pncxk_args *a) {
     switch (PNCX_KEY(xtype, itype)) {
 #define CASE(XT, IT) case PNCX_KEY(XT, IT): return put_one<XT, IT>(preserve, a);
-        PNCX_ALL_PAIRS(CASE)
+        PNCX_ROW(CASE, PNCX_XT)
 #undef CASE
         default: return NC_EBADTYPE;
     }
 }
 
-extern "C" int pncxk_batch_put(int xtype, int itype, int preserve, const pncxk_batch_args *a) {
+extern "C" int PNCX_FN(pncxk_batch_put)(int xtype, int itype, int preserve, const pncxk_batch_args *a) {
     switch (PNCX_KEY(xtype, itype)) {
 #define CASE(XT, IT) case PNCX_KEY(XT, IT): return put_batch<XT, IT>(preserve, a);
-        PNCX_ALL_PAIRS(CASE)
+        PNCX_ROW(CASE, PNCX_XT)
 #undef CASE
         default: return NC_EBADTYPE;
     }
 }
 
-extern "C" int pncxk_batch_fused_put(int xtype, int itype, int preserve, const pncxk_batch_args *a,
+extern "C" int PNCX_FN(pncxk_batch_fused_put)(int xtype, int itype, int preserve, const pncxk_batch_args *a,
                                      const pncxk_batch_args *m) {
     switch (PNCX_KEY(xtype, itype)) {
 #define CASE(XT, IT) case PNCX_KEY(XT, IT): return put_fused<XT, IT>(preserve, a, m);
-        PNCX_ALL_PAIRS(CASE)
+        PNCX_ROW(CASE, PNCX_XT)
 #undef CASE
         default: return NC_EBADTYPE;
     }
@@ -84,24 +96,19 @@ int put_imap(int preserve, const pncxk_args *a, const pncxk_imap *m) {
 }
 }  // namespace
 
-extern "C" int pncxk_imap_put(int xtype, int itype, int preserve, const pncxk_args *a, const pncxk_imap *m) {
+extern "C" int PNCX_FN(pncxk_imap_put)(int xtype, int itype, int preserve, const pncxk_args *a, const pncxk_imap *m) {
     switch (PNCX_KEY(xtype, itype)) {
 #define CASE(XT, IT) case PNCX_KEY(XT, IT): return put_imap<XT, IT>(preserve, a, m);
-        PNCX_ALL_PAIRS(CASE)
+        PNCX_ROW(CASE, PNCX_XT)
 #undef CASE
         default: return NC_EBADTYPE;
     }
 }
 
-extern "C" int pncxk_opinfo_get_get(int xtype, int itype, pncxk_opinfo *o);
-
-extern "C" int pncxk_opinfo_getput(int kind, int xtype, int itype, int preserve, pncxk_opinfo *o) {
-    (void)preserve;
-    if (kind == PNCXK_GET) return pncxk_opinfo_get_get(xtype, itype, o);
-    if (kind != PNCXK_PUT) return NC_EINVAL;
+extern "C" int PNCX_FN(pncxk_opinfo_put)(int xtype, int itype, pncxk_opinfo *o) {
     switch (PNCX_KEY(xtype, itype)) {
 #define CASE(XT, IT) case PNCX_KEY(XT, IT): return put_info<XT, IT>(o);
-        PNCX_ALL_PAIRS(CASE)
+        PNCX_ROW(CASE, PNCX_XT)
 #undef CASE
         default: return NC_EBADTYPE;
     }

@@ -502,6 +502,15 @@ int pncxrt_device_count(void) {
     return n;
 }
 int pncxrt_set_device(int dev) { return rt(hipSetDevice(dev), "hipSetDevice"); }
+// HIP loads a code object on a device at the first launch from it; a
+// function-attribute query loads it too.  This file's (the same-type swaps
+// and copies, the batch and fill kernels: 1.2 MB) costs 4-5 ms, which the
+// create/open warm-up (pncx_warmup) takes off a process's first put; the
+// per-type conversion objects stay lazy (~18 ms each, pncx_kern_xt.c)
+int pncxrt_load_swap_code(void) {
+    hipFuncAttributes fa;
+    return rt(hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&k_swap_generic)), "hipFuncGetAttributes");
+}
 int pncxrt_get_device(void) {
     int d = -1;
     if (hipGetDevice(&d) != hipSuccess) return -1;

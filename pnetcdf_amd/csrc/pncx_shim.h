@@ -193,6 +193,7 @@ long long pncx_knob(int id);
 int  pncxrt_device_count(void);
 int  pncxrt_set_device(int dev);
 int  pncxrt_get_device(void);
+int  pncxrt_load_swap_code(void);      /* the swap file's code object on the current device */
 int  pncxrt_malloc(void **p, size_t n);
 int  pncxrt_free(void *p);
 int  pncxrt_host_alloc(void **p, size_t n);
