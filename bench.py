@@ -691,6 +691,9 @@ def c1_first_touch(nrec=32, n=1 << 20, cpu=True):
                      "get_GiBps": round(xbytes / (o["get_ms_median"] * 1e-3) / GIB, 3)}
     out = {"pattern": f"benchmarks/C/pnetcdf_put_vara.c:193-209, one rank: record variable x(time, {n}) NC_INT, "
                       f"{nrec} records of 4 MiB each put once (appended) then got once; per-call medians",
+           "loops": "put_loop_ms / get_loop_ms: the whole loops as the reference's benchmark times its write loop, "
+                    "including the program's own update of each record's values (and, in device_buffers, its "
+                    "4 MiB hipMemcpy of them to the device)",
            "legs": legs}
     if refs:
         ok = [x for x in refs if x.get("check_ok")]
