@@ -106,7 +106,7 @@ static const char *const g_ph_names[PH_N] = {
 static const char *const g_knob_names[PNCXK_NKNOB] = {
     "TILE_U", "XPOSE_MERGE", "URUN", "TMAP_VEC", "IMAP_ROWS", "FUSE_LANES", "BATCH_FUSE", "TMAP_IMAP",
     "TOFF16", "TOFF_MAX_ELEMS", "XPOSE_ORDER", "TOFF_RUNS", "HOST_ZC", "IO_INLINE_MB", "FILE_WINDOW", "IO_POPULATE", "HOST_ZC_MAX_MB", "TGAP",
-    "GROW", "READ_SPLIT", "WARM", "PREALLOC"};
+    "GROW", "READ_SPLIT", "WARM"};
 static long long g_knob[PNCXK_NKNOB];
 
 long long pncx_knob(int id)

@@ -41,8 +41,7 @@ typedef struct task {
     struct task *next;
     pio_batch *b;
     int fd, write;                   /* write: 1 = pwrite, 2 = mmap + memcpy for large runs,
-                                      * 3 = one mapping per share over many small runs,
-                                      * 4 = allocate pages past EOF (pio_prealloc) */
+                                      * 3 = one mapping per share over many small runs */
     pio_run *runs;                   /* shared by the tasks of one job */
     size_t n;
     long long lo, hi;                /* byte range of the concatenated runs */
@@ -150,10 +149,6 @@ static int do_range(int fd, int write, const pio_run *runs, size_t n, long long 
     long long pos = 0;
     size_t i;
     int err = NC_NOERR;
-    if (write == 4) {                    /* pio_prealloc: pages only, the size stays */
-        (void)fallocate(fd, FALLOC_FL_KEEP_SIZE, (off_t)(runs[0].off + lo), (off_t)(hi - lo));
-        return NC_NOERR;
-    }
     if (write == 3) {
         if (span_write(fd, runs, n, lo, hi) == 0) return NC_NOERR;
         write = 1;
@@ -377,17 +372,6 @@ int pio_read_split(pio_batch *b, int fd, const pio_run *runs, size_t n, int part
         return err;
     }
     return queue_tasks(b, fd, 0, runs, n, total, parts);
-}
-
-int pio_prealloc(pio_batch *b, int fd, long long off, long long len)
-{
-    pio_run r;
-    if (len <= 0) return NC_NOERR;
-    (void)pio_threads();
-    r.off = off;
-    r.len = len;
-    r.mem = NULL;
-    return queue_tasks(b, fd, 4, &r, 1, len, 1);
 }
 
 int pio_wait(pio_batch *b)

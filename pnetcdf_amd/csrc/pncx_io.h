@@ -44,9 +44,6 @@ int  pio_threads(void);
 /* A read job split over up to `parts` pool threads whatever its size
  * (pieces of at least 64 KiB): the inline gets' chunks (pncx_nc.c). */
 int  pio_read_split(pio_batch *b, int fd, const pio_run *runs, size_t n, int parts);
-/* Allocate the pages of [off, off + len) on a pool thread without changing
- * the file's size (fallocate FALLOC_FL_KEEP_SIZE); pio_wait(b) waits for it. */
-int  pio_prealloc(pio_batch *b, int fd, long long off, long long len);
 
 
 int  pio_write_all(int fd, const void *buf, size_t n, long long off);

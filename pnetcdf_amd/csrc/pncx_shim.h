@@ -185,8 +185,6 @@ enum {
                                  * the GPU converts (tmpfs)                  */
     PNCXK_KNOB_READ_SPLIT,      /* pool preads per chunk of an inline get    */
     PNCXK_KNOB_WARM,            /* 0: no device/staging warm-up at create/open */
-    PNCXK_KNOB_PREALLOC,        /* 0: no allocation of the next append's pages
-                                 * past EOF after an appending put (tmpfs)   */
     PNCXK_NKNOB
 };
 long long pncx_knob(int id);

@@ -109,16 +109,14 @@ def _appends(gpu, path, xt, it, n, where, order):
 def test_appends_same_with_and_without_first_touch_paths(gpu, shm_dir, knob, xt, it, where):
     """records appended in order and with holes (3, 0, 5, 1): the same file
     bytes, statuses (NC_ERANGE included) and read-back values with the
-    appended-range allocation, the next append's preallocation and split
-    reads off and on, equal to the oracle; the file's size is the last
-    record's end"""
+    appended-range allocation and split reads off and on, equal to the
+    oracle; the file's size is the last record's end"""
     n = (1 << 18) + 7
     order = [3, 0, 5, 1]
     runs = {}
     for mode in (0, 1):
         knob("GROW", mode)
         knob("READ_SPLIT", 4 if mode else 0)
-        knob("PREALLOC", mode)
         runs[mode] = _appends(gpu, os.path.join(shm_dir, f"a{mode}.nc"), xt, it, n, where, order)
     assert runs[0][0] == runs[1][0], "file bytes differ"
     assert runs[0][1] == runs[1][1], "statuses or read-back values differ"
@@ -137,41 +135,3 @@ def test_appends_same_with_and_without_first_touch_paths(gpu, shm_dir, knob, xt,
     for r in (2, 4):                                 # never written: the holes read as zeros
         off = v["begin"] + r * xs * n
         assert raw[off:off + xs * n] == b"\0" * (xs * n)
-
-
-@pytest.mark.parametrize("where", ["host", "dev"])
-def test_prealloc_keeps_size_and_allocates_ahead(gpu, shm_dir, knob, where):
-    """after each appending put the next record's pages are allocated past
-    EOF (FALLOC_FL_KEEP_SIZE): the file's size is always the last record's
-    end, its allocated blocks run one record further, reads past the end stay
-    empty, and with PNCX_PREALLOC=0 nothing is allocated past the end"""
-    torch = gpu
-    n = (1 << 18) + 7
-    xs = 4
-    sizes = {}
-    for mode in (1, 0):
-        knob("PREALLOC", mode)
-        path = os.path.join(shm_dir, f"p{mode}.nc")
-        err, ncid = N.create(path, N.NC_64BIT_DATA)
-        assert err == 0
-        N.def_dim(ncid, "t", N.NC_UNLIMITED)
-        N.def_dim(ncid, "x", n)
-        N.def_var(ncid, "r", T.NC_INT, [0, 1])
-        assert N.enddef(ncid) == 0
-        for r in range(3):
-            b = np.arange(n, dtype=np.int32) + r
-            if where == "dev":
-                assert N.put_var_dev(ncid, 0, torch.from_numpy(b).cuda(), [r, 0], [1, n]) == 0
-            else:
-                assert N.put_var(ncid, 0, b, [r, 0], [1, n], itype=T.ITYPE_INT) == 0
-        assert N.close(ncid) == 0
-        st = os.stat(path)
-        h = cdfparse.parse_cdf(open(path, "rb").read())
-        end = h["vars"][0]["begin"] + 3 * xs * n
-        assert st.st_size == end and h["numrecs"] == 3
-        sizes[mode] = st.st_blocks * 512
-        with open(path, "rb") as fh:
-            fh.seek(end)
-            assert fh.read(16) == b""
-    assert sizes[1] >= sizes[0] + xs * n - 8192, sizes     # one record ahead (page rounding)
-    assert sizes[0] < os.path.getsize(os.path.join(shm_dir, "p0.nc")) + 2 * 4096, sizes
