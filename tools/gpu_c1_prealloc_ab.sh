@@ -3,6 +3,8 @@
 # whole processes alternating (an in-process alternation would hand the
 # preallocated pages of an "on" record to the next "off" record).
 #   bash tools/gpu_c1_prealloc_ab.sh [rounds]
+# (the preallocation and its knob were removed after this A/B, commit 676ec1c;
+# the script reproduces profiles/r05q_prealloc_ab.txt on 62480bf)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 F=/dev/shm/pncx_pre_ab.nc
