@@ -19,7 +19,7 @@
  *       config 1 under benchmarks/C/pnetcdf_put_vara.c's pattern: a record
  *       variable x(time, n) NC_INT, each record put once (appended), then
  *       each record got once; per-call medians, loop and close times.
- *   api_check c1ab <nc> <n> <nrec> <knob> <a> <b>
+ *   api_check c1ab <nc> <n> <nrec> <knob> <a> <b> [dev]
  *       c1first with a libpncx knob alternating between a and b record by
  *       record: put and get medians under each value (A/B in one process).
  *   api_check numrecs <nc>
@@ -466,9 +466,10 @@ static int mode_c1first(const char *path, MPI_Offset n, int nrec, int dev)
 /* c1first with a libpncx knob alternating between two values record by
  * record (A/B in one process, so both settings see the same box state):
  * medians of the puts and gets under each value */
-static int mode_c1ab(const char *path, MPI_Offset n, int nrec, const char *knob, long long va, long long vb)
+static int mode_c1ab(const char *path, MPI_Offset n, int nrec, const char *knob, long long va, long long vb, int dev)
 {
     int *h = (int *)malloc((size_t)n * 4), *g = (int *)calloc((size_t)n, 4), ncid, dimid[2], varid, r, bad = 0;
+    void *dh = dev ? to_dev(NULL, (size_t)n * 4) : NULL, *dg = dev ? to_dev(NULL, (size_t)n * 4) : NULL;
     double *tp[2], *tg[2], t0;
     int np[2] = {0, 0}, ng[2] = {0, 0}, k;
     int (*kset)(const char *, long long) = (int (*)(const char *, long long))dlsym(RTLD_DEFAULT, "pncx_knob_set");
@@ -487,10 +488,11 @@ static int mode_c1ab(const char *path, MPI_Offset n, int nrec, const char *knob,
     for (r = 0; r < nrec; r++) {
         k = (r / 2) % 2 ^ (r % 2);                      /* A B B A A B B A ...: no order bias */
         for (i = 0; i < n; i++) h[i] += 1;
+        if (dev && hipMemcpy(dh, h, (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess) { fprintf(stderr, "H2D failed\n"); exit(3); }
         start[0] = r;
         kset(knob, k ? vb : va);
         t0 = MPI_Wtime();
-        CHECK(ncmpi_put_vara_int_all(ncid, varid, start, count, h));
+        CHECK(ncmpi_put_vara_int_all(ncid, varid, start, count, dev ? dh : (void *)h));
         if (r > 0) tp[k][np[k]++] = MPI_Wtime() - t0;
     }
     for (i = 0; i < n; i++) h[i] -= nrec;
@@ -499,8 +501,9 @@ static int mode_c1ab(const char *path, MPI_Offset n, int nrec, const char *knob,
         start[0] = r;
         kset(knob, k ? vb : va);
         t0 = MPI_Wtime();
-        CHECK(ncmpi_get_vara_int_all(ncid, varid, start, count, g));
+        CHECK(ncmpi_get_vara_int_all(ncid, varid, start, count, dev ? dg : (void *)g));
         if (r > 0) tg[k][ng[k]++] = MPI_Wtime() - t0;
+        if (dev) from_dev(g, dg, (size_t)n * 4);
         for (i = 0; i < n && !bad; i++) bad = g[i] != h[i] + r + 1;
     }
     kset(knob, -1);
@@ -514,7 +517,8 @@ static int mode_c1ab(const char *path, MPI_Offset n, int nrec, const char *knob,
                1e3 * tg[k][ng[k] / 2]);
         free(tp[k]); free(tg[k]);
     }
-    printf(", \"errors\": %d}\n", nerrs);
+    printf(", \"dev\": %d, \"errors\": %d}\n", dev, nerrs);
+    if (dev) { hipFree(dh); hipFree(dg); }
     free(h); free(g);
     return nerrs != 0;
 }
@@ -889,7 +893,8 @@ int main(int argc, char **argv)
     else if (argc >= 6 && strcmp(argv[1], "c1first") == 0)
         rc = mode_c1first(argv[2], atoll(argv[3]), atoi(argv[4]), atoi(argv[5]));
     else if (argc >= 8 && strcmp(argv[1], "c1ab") == 0)
-        rc = mode_c1ab(argv[2], atoll(argv[3]), atoi(argv[4]), argv[5], atoll(argv[6]), atoll(argv[7]));
+        rc = mode_c1ab(argv[2], atoll(argv[3]), atoi(argv[4]), argv[5], atoll(argv[6]), atoll(argv[7]),
+                       argc >= 9 ? atoi(argv[8]) : 0);
     else if (argc >= 3 && strcmp(argv[1], "numrecs") == 0) rc = mode_numrecs(argv[2]);
     else if (argc >= 3 && strcmp(argv[1], "openfail") == 0) rc = mode_openfail(argv[2]);
     else if (argc >= 3 && strcmp(argv[1], "bputshort") == 0) rc = mode_bputshort(argv[2]);
