@@ -35,8 +35,11 @@ CASES = [
     ([200, 3, 130], [1, 200, 600]),   # 64 x 128 tiles: partial along U (72) and P (2)
     ([256, 2, 128], [1, 256, 512]),   # whole 64 x 128 tiles only
 ]
+# every external type at least once: one code object per type (pncx_kern_xt.c)
 PAIRS = [(T.NC_INT, T.ITYPE_DOUBLE), (T.NC_SHORT, T.ITYPE_FLOAT), (T.NC_DOUBLE, T.ITYPE_DOUBLE),
-         (T.NC_BYTE, T.ITYPE_INT), (T.NC_UINT64, T.ITYPE_SCHAR), (T.NC_FLOAT, T.ITYPE_FLOAT)]
+         (T.NC_BYTE, T.ITYPE_INT), (T.NC_UINT64, T.ITYPE_SCHAR), (T.NC_FLOAT, T.ITYPE_FLOAT),
+         (T.NC_UBYTE, T.ITYPE_USHORT), (T.NC_USHORT, T.ITYPE_INT), (T.NC_UINT, T.ITYPE_DOUBLE),
+         (T.NC_INT64, T.ITYPE_FLOAT)]
 
 
 @pytest.fixture(scope="module")

@@ -336,6 +336,48 @@ def test_dev_batch_mixed_classes(torch_cuda):
         assert buf.cpu().numpy()[:nb].tobytes() == exp
 
 
+XTYPES = [T.NC_BYTE, T.NC_UBYTE, T.NC_SHORT, T.NC_USHORT, T.NC_INT, T.NC_UINT, T.NC_FLOAT, T.NC_DOUBLE,
+          T.NC_INT64, T.NC_UINT64]
+
+
+@pytest.mark.parametrize("xt", XTYPES, ids=[T.XNAME[x] for x in XTYPES])
+def test_dev_batch_every_external_type(torch_cuda, xt):
+    """The conversion kernels are one code object per external type
+    (pncx_kern_xt.c dispatches): a batch of get and put segments of this
+    type with three converting internal types, each against the oracle, so
+    every type's batch entry points run (the per-pair tests cover pncxk_get
+    and pncxk_put)."""
+    torch = torch_cuda
+    from pnetcdf_amd import pncx
+    ora = OracleConv()
+    rng = np.random.default_rng(0xB7 + xt)
+    its = [i for i in (T.ITYPE_DOUBLE, T.ITYPE_FLOAT, T.ITYPE_INT, T.ITYPE_SCHAR) if T.XNAME[xt] != T.INAME[i]][:3]
+    segs, refs = [], []
+    for d in (T.PNCX_GET, T.PNCX_PUT):
+        for it in its:
+            n = int(rng.integers(1000, 30000))
+            raw = rng.integers(0, 256, n * 8 + 8, dtype=np.uint8)
+            if d == T.PNCX_GET:
+                xin = raw[: n * T.xlen(xt)].tobytes()
+                exp, so = ora.getn(5, xt, xin, it)
+                dx = torch.from_numpy(np.frombuffer(xin + b"\0" * 16, np.uint8).copy()).cuda()
+                di = torch.zeros(n * T.ilen(it) + 16, dtype=torch.uint8, device="cuda")
+                refs.append((di, exp.tobytes(), so, n * T.ilen(it)))
+            else:
+                ib = np.frombuffer(raw.tobytes(), T.ITYPE_NP[it])[:n].copy()
+                xb, so = ora.putn(5, xt, ib, it, T.fill_bytes(xt))
+                di = torch.from_numpy(np.frombuffer(ib.tobytes() + b"\0" * 16, np.uint8).copy()).cuda()
+                dx = torch.zeros(n * T.xlen(xt) + 16, dtype=torch.uint8, device="cuda")
+                refs.append((dx, xb, so, n * T.xlen(xt)))
+            segs.append(dict(dir=d, cdf_ver=5, xtype=xt, itype=it, nelems=n, xbuf=dx, ibuf=di,
+                             fill=T.fill_bytes(xt) if d == T.PNCX_PUT else None))
+    st = pncx.dev_batch(segs)
+    torch.cuda.synchronize()
+    for (buf, exp, so, nb), stv in zip(refs, st):
+        assert stv == so
+        assert buf.cpu().numpy()[:nb].tobytes() == exp
+
+
 def test_dev_batch_plan_cache_statuses(torch_cuda):
     """A repeated segment list reuses the device plan (no upload); statuses
     carry a per-call epoch, so they follow each call's data and never report
