@@ -48,6 +48,24 @@ def test_pncx_h_symbols_exported(built):
     assert not missing, missing
 
 
+def test_conversion_kernels_one_object_per_external_type(built):
+    """pncx_kern_put.hip / pncx_kern_get.hip are compiled once per external
+    type (Makefile XTS, round 5): every one of the ten types has its put, get,
+    batch, fused-batch, imap and opinfo launchers in libpncx.so, and the
+    library holds 2 x 10 + 2 gfx950 code objects (swap, diff), so a process
+    loads only the types it converts"""
+    syms = exported(LIB)
+    xts = [T.NC_BYTE, T.NC_SHORT, T.NC_INT, T.NC_FLOAT, T.NC_DOUBLE, T.NC_UBYTE, T.NC_USHORT, T.NC_UINT,
+           T.NC_INT64, T.NC_UINT64]
+    fams = ["pncxk_put", "pncxk_batch_put", "pncxk_batch_fused_put", "pncxk_imap_put", "pncxk_opinfo_put",
+            "pncxk_get", "pncxk_batch_get", "pncxk_batch_fused_get", "pncxk_imap_get", "pncxk_opinfo_get_get"]
+    missing = [f"{f}_x{x}" for f in fams for x in xts if f"{f}_x{x}" not in syms]
+    assert not missing, missing
+    assert not [s for s in syms if s.startswith("pncxk_put_x") and s not in {f"pncxk_put_x{x}" for x in xts}]
+    from tests.test_isa_store_hazard import code_objects
+    assert len(code_objects(LIB)) == 22
+
+
 def test_pncx_nc_h_symbols_exported(built):
     """file-level API (include/pncx_nc.h)"""
     decl = declared("pncx_nc.h")
