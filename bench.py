@@ -634,21 +634,61 @@ def c1_reference_sequence(path, var_offset, reps=21, n=1 << 20):
     return out
 
 
-def c1_first_touch(nrec=32, n=1 << 20, cpu=True):
+C1_LEGS = (("host_8_io_threads", 0, None), ("host_1_io_thread", 0, "1"), ("device_buffers", 1, None))
+
+
+def c1_first_order(reps):
+    """Interleaved run order of the first-touch legs: the reference's
+    sequence, then every library leg, `reps` times over, closing with the
+    reference again -- so each library run has a reference run on both sides
+    of it, and no leg always runs first."""
+    order = []
+    for k in range(reps):
+        order.append("ref")
+        legs = [name for name, _, _ in C1_LEGS]
+        order += legs[k % len(legs):] + legs[:k % len(legs)]     # rotate which leg follows the reference
+    return order + ["ref"]
+
+
+def c1_first_compare(order, runs):
+    """Per library run, its put/get/loop ratios against the mean of the two
+    reference runs that bracket it in `order` (the nearest before and after).
+    `runs` holds one result dict per entry of `order`."""
+    for i, key in enumerate(order):
+        r = runs[i]
+        if key == "ref" or "put_ms" not in r:
+            continue
+        near = []
+        for j in list(range(i - 1, -1, -1)) + list(range(i + 1, len(order))):
+            if order[j] == "ref" and runs[j].get("check_ok") and (not near or (j > i) != (near[0] > i)):
+                near.append(j)
+            if len(near) == 2:
+                break
+        if not near:
+            continue
+        ref = {k: sum(runs[j][k] for j in near) / len(near) for k in ("put_ms", "get_ms", "put_loop_ms")}
+        r["put_vs_reference"] = round(ref["put_ms"] / r["put_ms"], 3)
+        r["get_vs_reference"] = round(ref["get_ms"] / r["get_ms"], 3)
+        r["put_loop_vs_reference"] = round(ref["put_loop_ms"] / r["put_loop_ms"], 3)
+
+
+def c1_first_touch(nrec=32, n=1 << 20, cpu=True, reps=2):
     """C1 under the reference's own benchmark pattern
     (benchmarks/C/pnetcdf_put_vara.c:193-209): a record variable x(time, n)
     NC_INT, each 4 MiB record put exactly once with ncmpi_put_vara_int_all
     (appended past the end of the file) and then got once
-    (tests/mpi/api_check c1first), per-call medians; beside it the
-    reference's sequence on the same records in the same run
-    (oracle/ref_sequence.c orc_c1_first_sequence: swap, pwrite, swap back,
-    numrecs; malloc xbuf, pread, swap, memcpy, free), timed before and after
-    the library's legs."""
+    (tests/mpi/api_check c1first, with PNCX_PHASES=1 for the per-phase
+    host time of the puts and gets), per-call medians; beside it the
+    reference's sequence on the same records (oracle/ref_sequence.c
+    orc_c1_first_sequence: swap, pwrite, swap back, numrecs; malloc xbuf,
+    pread, swap, memcpy, free).  The legs and the reference runs are
+    interleaved (c1_first_order) and every library leg runs `reps` times;
+    each run is compared with the reference runs on either side of it."""
     exe = os.path.join(ROOT, "tests", "mpi", "api_check")
     shm = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
     path = os.path.join(shm, f"pncx_c1first_{os.getpid()}.nc")
-    xbytes = 4.0 * n
-    legs, refs, rec_offset = {}, [], None
+    legs_by = {name: (dev, th) for name, dev, th in C1_LEGS}
+    rec_offset = [None]
 
     def ref_run():
         from oracle import oracle as O
@@ -656,64 +696,85 @@ def c1_first_touch(nrec=32, n=1 << 20, cpu=True):
         lib.orc_c1_first_sequence.argtypes = [ctypes.c_char_p, ctypes.c_longlong, ctypes.c_longlong, ctypes.c_int,
                                               ctypes.POINTER(ctypes.c_double)]
         lib.orc_c1_first_sequence.restype = ctypes.c_int
+        if rec_offset[0] is None:               # the library's header length for this variable
+            rec_offset[0] = lib_run("host_1_io_thread", probe=True).get("rec_offset")
         o = (ctypes.c_double * 6)()
-        rc = lib.orc_c1_first_sequence(path.encode(), rec_offset, n, nrec, o)
+        rc = lib.orc_c1_first_sequence(path.encode(), rec_offset[0], n, nrec, o)
         return {"check_ok": rc == 0, "error": rc} if rc else {
             "check_ok": True, "put_ms": round(o[0], 4), "get_ms": round(o[1], 4), "put_ms_min": round(o[2], 4),
             "get_ms_min": round(o[3], 4), "put_loop_ms": round(o[4], 3), "get_loop_ms": round(o[5], 3)}
 
-    order = [("host_8_io_threads", 0, None), ("ref", None, None), ("host_1_io_thread", 0, "1"),
-             ("device_buffers", 1, None), ("ref", None, None)]
-    for key, dev, threads in order:
-        if key == "ref":
-            if cpu and rec_offset is not None:
-                refs.append(ref_run())
-            continue
+    def lib_run(key, probe=False):
+        dev, threads = legs_by[key]
         env = dict(os.environ)
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        env["PNCX_PHASES"] = "1"
         if threads is not None:
             env["PNCX_IO_THREADS"] = threads
-        r = subprocess.run([exe, "c1first", path, str(n), str(nrec), str(dev)], capture_output=True, text=True,
-                           timeout=300, env=env)
+        r = subprocess.run([exe, "c1first", path, str(n), str(2 if probe else nrec), str(dev)],
+                           capture_output=True, text=True, timeout=300, env=env)
         if r.returncode != 0:
-            legs[key] = {"error": r.returncode, "stderr": r.stderr[-400:]}
-            continue
+            return {"error": r.returncode, "stderr": r.stderr[-400:]}
         o = json.loads(r.stdout.strip().splitlines()[-1])
-        rec_offset = o["rec_offset"]
-        legs[key] = {"put_ms": o["put_ms_median"], "get_ms": o["get_ms_median"], "put_ms_min": o["put_ms_min"],
-                     "get_ms_min": o["get_ms_min"], "put_loop_ms": o["put_loop_ms"], "get_loop_ms": o["get_loop_ms"],
-                     "close_ms": o["close_ms"], "errors": o["errors"],
-                     # the first put of the process and create..enddef, where the
-                     # library's one-time setup now runs
-                     "put_first_ms": o.get("put_first_ms"), "get_first_ms": o.get("get_first_ms"),
-                     "create_to_enddef_ms": o.get("create_to_enddef_ms"),
-                     "put_GiBps": round(xbytes / (o["put_ms_median"] * 1e-3) / GIB, 3),
-                     "get_GiBps": round(xbytes / (o["get_ms_median"] * 1e-3) / GIB, 3)}
+        if probe:
+            return o
+        rec_offset[0] = o["rec_offset"]
+        ph = o.get("put_phases", {})
+        return {"put_ms": o["put_ms_median"], "get_ms": o["get_ms_median"], "put_ms_min": o["put_ms_min"],
+                "get_ms_min": o["get_ms_min"], "put_loop_ms": o["put_loop_ms"], "get_loop_ms": o["get_loop_ms"],
+                "close_ms": o["close_ms"], "errors": o["errors"],
+                # the first put of the process and create..enddef, where the
+                # library's one-time setup runs
+                "put_first_ms": o.get("put_first_ms"), "get_first_ms": o.get("get_first_ms"),
+                "create_to_enddef_ms": o.get("create_to_enddef_ms"),
+                # us per put after the first, by phase (pncx_phase_name)
+                "put_phases_us": {k.split(".", 1)[1]: v[0] for k, v in ph.items() if k.startswith("put.")},
+                "put_phases": ph, "first_put_phases": o.get("first_put_phases"),
+                "get_phases": o.get("get_phases")}
+
+    order = [k for k in c1_first_order(reps) if cpu or k != "ref"]
+    runs = []
+    for key in order:
+        runs.append(ref_run() if key == "ref" else lib_run(key))
+    c1_first_compare(order, runs)
     out = {"pattern": f"benchmarks/C/pnetcdf_put_vara.c:193-209, one rank: record variable x(time, {n}) NC_INT, "
                       f"{nrec} records of 4 MiB each put once (appended) then got once; per-call medians",
            "loops": "put_loop_ms / get_loop_ms: the whole loops as the reference's benchmark times its write loop, "
                     "including the program's own update of each record's values (and, in device_buffers, its "
                     "4 MiB hipMemcpy of them to the device)",
-           "legs": legs}
-    if refs:
-        ok = [x for x in refs if x.get("check_ok")]
-        out["reference_sequence"] = {"runs": refs, "cores": 1, "kind": "port",
-                                     "sample": "oracle/ref_sequence.c orc_c1_first_sequence on the same file and "
-                                               "records, timed before and after the library's legs"}
-        if ok:
-            rp = sum(x["put_ms"] for x in ok) / len(ok)
-            rg = sum(x["get_ms"] for x in ok) / len(ok)
-            out["reference_sequence"].update({"put_ms": round(rp, 4), "get_ms": round(rg, 4)})
-            for key, leg in legs.items():
-                if "put_ms" in leg:
-                    leg["put_vs_reference"] = round(rp / leg["put_ms"], 3)
-                    leg["get_vs_reference"] = round(rg / leg["get_ms"], 3)
-    out["check_ok"] = all(v.get("errors", 1) == 0 for v in legs.values()) and all(x.get("check_ok") for x in refs)
+           "order": order, "runs": runs}
+    out["check_ok"] = all((r.get("check_ok") if k == "ref" else r.get("errors", 1) == 0)
+                          for k, r in zip(order, runs))
     try:
         os.unlink(path)
     except OSError:
         pass
     return out
+
+
+def c1_first_summary(ft):
+    """The compact form of c1_first_touch's result for the printed line: per
+    leg, every run's put/get medians, loop time and its ratios against the
+    bracketing reference runs, and the put's phase means of the first run."""
+    legs = {}
+    for key, r in zip(ft["order"], ft["runs"]):
+        name = "reference_sequence" if key == "ref" else key
+        s = legs.setdefault(name, {})
+        if "put_ms" not in r:
+            s.setdefault("errors", []).append(r.get("error"))
+            continue
+        fields = ["put_ms", "get_ms", "put_loop_ms"]
+        if key != "ref":
+            fields += ["put_vs_reference", "get_vs_reference", "put_loop_vs_reference"]
+        for f in fields:
+            if f in r:
+                s.setdefault(f, []).append(round(r[f], 3))
+        if key != "ref" and "put_phases_us" in r and "put_phases_us" not in s:
+            s["put_phases_us"] = {k: round(v) for k, v in r["put_phases_us"].items() if v >= 5}
+    for name, s in legs.items():
+        if s.get("put_ms"):
+            s["put_ms_min_med_max"] = [min(s["put_ms"]), sorted(s["put_ms"])[len(s["put_ms"]) // 2], max(s["put_ms"])]
+    return {"legs": legs, "check_ok": ft["check_ok"], "runs_in_order": " ".join(ft["order"])}
 
 
 def c1_workload(cpu=True):
@@ -737,9 +798,95 @@ def c1_workload(cpu=True):
         os.unlink(path)
     except OSError:
         pass
-    res["first_touch"] = c1_first_touch(cpu=cpu)
-    out["check_ok"] = ok and res["first_touch"]["check_ok"]
+    out["first_touch"] = c1_first_touch(cpu=cpu)
+    out["check_ok"] = ok and out["first_touch"]["check_ok"]
     return out
+
+
+# --------------------------------------------------------------- the printed line
+DETAIL_PATH = os.path.join("profiles", "bench_detail_last.json")
+LINE_MAX_CHARS = 6000          # the driver keeps the last ~8 KB of stdout+stderr
+
+
+def _cpu_short(cb, head=True):
+    if not isinstance(cb, dict):
+        return cb
+    return {k: cb[k] for k in (("value", "unit") if head else ("value",)) + ("cores", "kind", "put_ms", "get_ms")
+            if k in cb}
+
+
+def _roof_short(rf, head=True):
+    if not isinstance(rf, dict):
+        return rf
+    keys = ("bound", "peak", "unit") if head else ()
+    out = {k: rf[k] for k in keys + ("achieved", "frac", "traffic", "kernel", "kernel_ms_avg", "call_ms_avg")
+           if k in rf}
+    ts = rf.get("traffic_source")
+    if isinstance(ts, dict):
+        out["traffic_source"] = f"{ts.get('file')} round {ts.get('round')}"
+    return out
+
+
+def compact_line(full, detail_path=DETAIL_PATH):
+    """The one JSON line rank 0 prints: the contract's keys and, per extra
+    workload, its rate, roofline and CPU baseline -- everything else of the
+    run (sample descriptions, C1's per-run phase breakdowns, rank lists) goes
+    to `detail_path`, named in the line.  Kept under LINE_MAX_CHARS so the
+    driver's captured tail holds every workload (BENCH_r05 lost C3 and C4 to
+    a 10.8 KB line)."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "slab_GiBps", "check_ok")
+    line = {k: full[k] for k in keep if k in full}
+    cfg = full.get("config", {})
+    line["config"] = {k: cfg[k] for k in ("workload", "slab_gib_per_gpu", "elements_per_gpu", "records_per_gpu",
+                                          "parallelism") if k in cfg}
+    line["roofline"] = _roof_short(full.get("roofline"))
+    line["cpu_baseline"] = _cpu_short(full.get("cpu_baseline"))
+    if full.get("cpu_baseline_all_cores"):
+        line["cpu_baseline_all_cores"] = _cpu_short(full["cpu_baseline_all_cores"])
+    line["check"] = full.get("check", "")[:160]
+    wls = {}
+    for name, w in full.get("workloads", {}).items():
+        if name == "c1":
+            c = {k: w[k] for k in ("value", "unit", "ms_per_step", "check_ok") if k in w}
+            h = w.get("legs", {})
+            c["repeated_range"] = {k: {f: v[f] for f in ("put_ms", "get_ms") if f in v}
+                                   for k, v in h.items() if isinstance(v, dict)}
+            c["cpu_baseline"] = _cpu_short(w.get("cpu_baseline"), head=False)
+            if "first_touch" in w:
+                c["first_touch"] = c1_first_summary(w["first_touch"])
+            wls[name] = c
+            continue
+        c = {k: w[k] for k in ("value", "ms_per_step", "steps", "n_gpus", "check_ok", "kernel_ms_per_rank")
+             if k in w}
+        c["roofline"] = _roof_short(w.get("roofline"), head=False)
+        c["cpu_baseline"] = _cpu_short(w.get("cpu_baseline"), head=False)
+        if w.get("cpu_baseline_all_cores"):
+            c["cpu_baseline_all_cores"] = _cpu_short(w["cpu_baseline_all_cores"], head=False)
+        wls[name] = c
+    if wls:
+        line["workloads"] = wls
+    if "gather" in full:
+        g = full["gather"]
+        line["gather"] = {k: g[k] for k in ("collective", "bytes_per_rank", "chunks", "ms", "GBps_into_rank0",
+                                            "checksums_ok", "via_xgmi") if k in g}
+    if "ranks" in full:
+        line["ranks"] = full["ranks"]
+    line["detail"] = detail_path
+    return line
+
+
+def emit(full):
+    """Write the whole result to DETAIL_PATH (best effort) and print the
+    compact line."""
+    try:
+        with open(os.path.join(ROOT, DETAIL_PATH), "w") as f:
+            json.dump(full, f, indent=1)
+    except OSError:
+        pass
+    s = json.dumps(compact_line(full))
+    print(s, flush=True)
+    return s
 
 
 def add_cpu_baselines(wls, budget):
@@ -901,7 +1048,7 @@ def worker(args):
             line["gather"] = gather
         if ranks is not None:
             line["ranks"] = ranks
-        print(json.dumps(line), flush=True)
+        emit(line)
     if dist is not None:
         dist.destroy_process_group()
     return 0

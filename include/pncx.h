@@ -381,6 +381,15 @@ int  pncx_get_device(void);
  * equivalent; ncmpi_create/ncmpi_open run it on a thread, pncx_nc.c
  * warm_start).  NC_NOERR or PNCX_EDEVICE. */
 int  pncx_warmup(void);
+/* Load on device `dev` the put and get conversion kernels of the external
+ * types in `mask` (bit x = NC type x; NC_CHAR ignored), each type once per
+ * device: 9-16 ms per type that the first put or get of the type would pay.
+ * ncmpi_enddef runs it on a thread for the types of the defined variables
+ * (pncx_nc.c, PNCX_PRELOAD=0 turns that off).  No reference equivalent.
+ * NC_NOERR or PNCX_EDEVICE.  pncx_preload_pending: the types of `mask`
+ * not loaded on `dev` yet. */
+int  pncx_preload_xtypes(int dev, unsigned mask);
+unsigned pncx_preload_pending(int dev, unsigned mask);
 /* Pin a long-lived host buffer for direct DMA (no reference equivalent: the
  * xbuf of ncmpio_getput.m4:216,422 is malloc'ed per call).  Host entry points
  * pin buffers >= 64 MiB themselves for the duration of a call; a buffer

@@ -20,6 +20,7 @@
  * with m4 (ITYPE_LIST, var_getput.m4:419-424, 810-816, 989-996).
  */
 #include <errno.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -63,24 +64,46 @@ PNC_driver *pncx_set_driver(PNC_driver *driver)
     return old;
 }
 
+/* The ncid table is shared by every thread of the process.  The reference
+ * guards it with a mutex when built with PNETCDF_THREAD_SAFE (file.c:30-33,
+ * new_id_PNCList :621-648, del_from_PNCList :655-674, PNC_check_id
+ * :681-703); here the mutex is always on -- the library itself runs
+ * threads (warm-up, preload, I/O pool), and tests/mpi/api_check pthread
+ * restates the reference's tst_pthread.c on it. */
+static pthread_mutex_t pnc_lock = PTHREAD_MUTEX_INITIALIZER;
+
 /* PNC_check_id (file.c) */
 static int PNC_check_id(int ncid, PNC **pncp)
 {
-    if (ncid < 0 || ncid >= NC_MAX_NFILES || pnc_list[ncid] == NULL) return NC_EBADID;
-    *pncp = pnc_list[ncid];
-    return NC_NOERR;
+    int err = NC_NOERR;
+    if (ncid < 0 || ncid >= NC_MAX_NFILES) return NC_EBADID;
+    pthread_mutex_lock(&pnc_lock);
+    if (pnc_list[ncid] == NULL) err = NC_EBADID;
+    else *pncp = pnc_list[ncid];
+    pthread_mutex_unlock(&pnc_lock);
+    return err;
 }
 
 static int new_id(PNC *p, int *ncidp)
 {
-    int i;
+    int i, err = NC_ENFILE;
+    pthread_mutex_lock(&pnc_lock);
     for (i = 0; i < NC_MAX_NFILES; i++)
         if (pnc_list[i] == NULL) {
             pnc_list[i] = p;
             *ncidp = i;
-            return NC_NOERR;
+            err = NC_NOERR;
+            break;
         }
-    return NC_ENFILE;
+    pthread_mutex_unlock(&pnc_lock);
+    return err;
+}
+
+static void del_id(int ncid)
+{
+    pthread_mutex_lock(&pnc_lock);
+    pnc_list[ncid] = NULL;
+    pthread_mutex_unlock(&pnc_lock);
 }
 
 static void free_pnc(PNC *p)
@@ -365,7 +388,7 @@ int ncmpi_create(MPI_Comm comm, const char *path, int cmode, MPI_Info info, int 
     err = driver->create(p->comm, p->path, cmode, *ncidp, env_mode, info, no_ina(), &ncp);
     if (status == NC_NOERR) status = err;
     if (err != NC_NOERR) {
-        pnc_list[*ncidp] = NULL;
+        del_id(*ncidp);
         *ncidp = -1;
         free_pnc(p);
         return status;
@@ -415,7 +438,7 @@ int ncmpi_open(MPI_Comm comm, const char *path, int omode, MPI_Info info, int *n
     err = driver->open(p->comm, p->path, omode, *ncidp, env_mode, info, no_ina(), &ncp);
     if (status == NC_NOERR) status = err;
     if (err != NC_NOERR) {
-        pnc_list[*ncidp] = NULL;
+        del_id(*ncidp);
         *ncidp = -1;
         free_pnc(p);
         return status;
@@ -429,7 +452,7 @@ int ncmpi_open(MPI_Comm comm, const char *path, int omode, MPI_Info info, int *n
     for (i = 0; i < nvars && !err; i++) err = add_var(p, i);
     if (err) {
         driver->close(ncp);
-        pnc_list[*ncidp] = NULL;
+        del_id(*ncidp);
         *ncidp = -1;
         free_pnc(p);
         return err;
@@ -443,7 +466,7 @@ int ncmpi_close(int ncid)
     int err = PNC_check_id(ncid, &p);
     if (err) return err;
     err = p->driver->close(p->ncp);
-    pnc_list[ncid] = NULL;          /* removed even on error (file.c:1716) */
+    del_id(ncid);                   /* removed even on error (file.c:1716) */
     free_pnc(p);
     return err;
 }
@@ -454,7 +477,7 @@ int ncmpi_abort(int ncid)
     int err = PNC_check_id(ncid, &p);
     if (err) return err;
     err = p->driver->abort(p->ncp);
-    pnc_list[ncid] = NULL;
+    del_id(ncid);
     free_pnc(p);
     return err;
 }
@@ -698,11 +721,13 @@ int ncmpi_inq_files_opened(int *num, int *ncids)
     int i;
     if (num == NULL) return NC_EINVAL;
     *num = 0;
+    pthread_mutex_lock(&pnc_lock);
     for (i = 0; i < NC_MAX_NFILES; i++)
         if (pnc_list[i] != NULL) {
             if (ncids != NULL) ncids[*num] = i;
             (*num)++;
         }
+    pthread_mutex_unlock(&pnc_lock);
     return NC_NOERR;
 }
 

@@ -100,13 +100,13 @@ static const char *const g_ph_names[PH_N] = {
     "put.plan", "put.register", "put.convert", "put.write", "put.wait", "put.unregister", "put.total",
     "get.plan", "get.register", "get.read", "get.convert", "get.unregister", "get.total",
     "conv.lock_pin", "conv.enqueue", "conv.sync", "conv.status", "conv.unpin",
-    "gpu.h2d", "gpu.kernel", "gpu.d2h", "file.window_map", "file.window_use", "put.grow", "warm"};
+    "gpu.h2d", "gpu.kernel", "gpu.d2h", "file.window_map", "file.window_use", "put.grow", "warm", "preload"};
 
 /* A/B knobs (pncx_shim.h): the environment once at load, then pncx_knob_set */
 static const char *const g_knob_names[PNCXK_NKNOB] = {
     "TILE_U", "XPOSE_MERGE", "URUN", "TMAP_VEC", "IMAP_ROWS", "FUSE_LANES", "BATCH_FUSE", "TMAP_IMAP",
     "TOFF16", "TOFF_MAX_ELEMS", "XPOSE_ORDER", "TOFF_RUNS", "HOST_ZC", "IO_INLINE_MB", "FILE_WINDOW", "IO_POPULATE", "HOST_ZC_MAX_MB", "TGAP",
-    "GROW", "READ_SPLIT", "WARM"};
+    "GROW", "READ_SPLIT", "WARM", "PRELOAD", "FAULT"};
 static long long g_knob[PNCXK_NKNOB];
 
 long long pncx_knob(int id)
@@ -662,6 +662,44 @@ int pncx_warmup(void)
     pthread_mutex_unlock(&c->lock);
     if (!err && pncxrt_load_swap_code() != 0) err = PNCX_EDEVICE;
     return err;
+}
+
+/* The put and get code objects of the external types in `mask` (bit x =
+ * NC type x) on device `dev`, each loaded once per device: 9-16 ms apiece,
+ * which the first put or get of a new type paid inside the call
+ * (profiles/r05p_first_call.txt).  The file layer runs this on a thread at
+ * enddef, where the defined variables' types are known (pncx_nc.c). */
+static unsigned g_loaded_xt[MAX_DEV];
+static pthread_mutex_t g_load_lock = PTHREAD_MUTEX_INITIALIZER;
+int pncx_preload_xtypes(int dev, unsigned mask)
+{
+    int x, err = 0;
+    if (dev < 0 || dev >= MAX_DEV || !have_device() || pncxrt_set_device(dev) != 0) return PNCX_EDEVICE;
+    for (x = 1; x < 32 && !err; x++) {
+        unsigned have;
+        if (!(mask & (1u << x)) || x == NC_CHAR) continue;
+        pthread_mutex_lock(&g_load_lock);
+        have = g_loaded_xt[dev];
+        pthread_mutex_unlock(&g_load_lock);
+        if (have & (1u << x)) continue;
+        err = pncxk_load_xtype(x);
+        if (err == NC_EBADTYPE) { err = 0; continue; }
+        pthread_mutex_lock(&g_load_lock);
+        if (!err) g_loaded_xt[dev] |= 1u << x;
+        pthread_mutex_unlock(&g_load_lock);
+    }
+    return err;
+}
+
+/* the types of `mask` not yet loaded on device `dev` */
+unsigned pncx_preload_pending(int dev, unsigned mask)
+{
+    unsigned have;
+    if (dev < 0 || dev >= MAX_DEV) return 0;
+    pthread_mutex_lock(&g_load_lock);
+    have = g_loaded_xt[dev];
+    pthread_mutex_unlock(&g_load_lock);
+    return mask & ~have & ~(1u << NC_CHAR);
 }
 
 /* elements per chunk for a call of n elements: about 4 chunks, each of

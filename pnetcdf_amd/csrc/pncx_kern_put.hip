@@ -113,3 +113,14 @@ extern "C" int PNCX_FN(pncxk_opinfo_put)(int xtype, int itype, pncxk_opinfo *o) 
         default: return NC_EBADTYPE;
     }
 }
+
+// A kernel of this file's code object, launched never: a function-attribute
+// query on it makes HIP load the object on the current device, which
+// pncx_preload_xtypes does at enddef for the types a file defines
+// (pncx_nc.c), off the first data call.
+__global__ void PNCX_FN(k_put_object)() {}
+extern "C" int PNCX_FN(pncxk_load_put)(void) {
+    hipFuncAttributes fa;
+    return hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&PNCX_FN(k_put_object))) == hipSuccess
+               ? 0 : PNCX_EDEVICE;
+}

@@ -26,7 +26,9 @@
     int pncxk_batch_get_x##X(int, int, const pncxk_batch_args *);                                      \
     int pncxk_batch_fused_get_x##X(int, int, const pncxk_batch_args *, const pncxk_batch_args *);      \
     int pncxk_imap_get_x##X(int, int, const pncxk_args *, const pncxk_imap *);                         \
-    int pncxk_opinfo_get_get_x##X(int, int, pncxk_opinfo *);
+    int pncxk_opinfo_get_get_x##X(int, int, pncxk_opinfo *);                                          \
+    int pncxk_load_put_x##X(void);                                                                     \
+    int pncxk_load_get_x##X(void);
 PNCX_XTS(DECL)
 #undef DECL
 
@@ -111,6 +113,15 @@ int pncxk_opinfo_getput(int kind, int xtype, int itype, int preserve, pncxk_opin
     }
     if (kind != PNCXK_PUT) return NC_EINVAL;
 #define C(X) case X: return pncxk_opinfo_put_x##X(xtype, itype, o);
+    SWITCH(C)
+#undef C
+}
+
+/* load the put and get code objects of one external type on the current
+ * device (pncx_preload_xtypes) */
+int pncxk_load_xtype(int xtype)
+{
+#define C(X) case X: { const int e = pncxk_load_put_x##X(); return e ? e : pncxk_load_get_x##X(); }
     SWITCH(C)
 #undef C
 }

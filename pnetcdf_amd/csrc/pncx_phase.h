@@ -36,6 +36,7 @@ enum {
     PH_WIN_USE,         /* a request converted through a file window       */
     PH_PUT_GROW,        /* appended pages allocated while the GPU converts */
     PH_WARM,            /* the create/open warm-up thread, start to end    */
+    PH_PRELOAD,         /* enddef: code objects of the defined types        */
     PH_N
 };
 

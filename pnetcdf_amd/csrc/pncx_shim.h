@@ -185,6 +185,8 @@ enum {
                                  * the GPU converts (tmpfs)                  */
     PNCXK_KNOB_READ_SPLIT,      /* pool preads per chunk of an inline get    */
     PNCXK_KNOB_WARM,            /* 0: no device/staging warm-up at create/open */
+    PNCXK_KNOB_PRELOAD,         /* 0: no code-object preload of the file's types at enddef */
+    PNCXK_KNOB_FAULT,           /* test only: 1 fails an appending put right after its grow */
     PNCXK_NKNOB
 };
 long long pncx_knob(int id);
@@ -194,6 +196,7 @@ int  pncxrt_device_count(void);
 int  pncxrt_set_device(int dev);
 int  pncxrt_get_device(void);
 int  pncxrt_load_swap_code(void);      /* the swap file's code object on the current device */
+int  pncxk_load_xtype(int xtype);      /* one external type's put + get code objects (pncx_kern_xt.c) */
 int  pncxrt_malloc(void **p, size_t n);
 int  pncxrt_free(void *p);
 int  pncxrt_host_alloc(void **p, size_t n);

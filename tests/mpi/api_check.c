@@ -15,10 +15,11 @@
  *       config 1 timed: reps x ncmpi_put_vara_int_all, then reps x
  *       ncmpi_get_vara_int_all of 1-D NC_INT x(n) on one open file (host or
  *       hipMalloc'ed buffers); prints median/min ms and the variable's offset.
- *   api_check c1first <nc> <n> <nrec> <dev>
+ *   api_check c1first <nc> <n> <nrec> <dev> [double]
  *       config 1 under benchmarks/C/pnetcdf_put_vara.c's pattern: a record
  *       variable x(time, n) NC_INT, each record put once (appended), then
  *       each record got once; per-call medians, loop and close times.
+ *       double: through ncmpi_put/get_vara_double_all (cross-type).
  *   api_check c1ab <nc> <n> <nrec> <knob> <a> <b> [dev]
  *       c1first with a libpncx knob alternating between a and b record by
  *       record: put and get medians under each value (A/B in one process).
@@ -53,11 +54,23 @@
  *   api_check header <nc> [nranks-agnostic]
  *       define-mode only (dims, variables, text attributes) on N ranks: the
  *       header rank 0 writes must not depend on N.
+ *   api_check pthread <prefix> <nthreads> <nx> <ny> <coll> [dev]
+ *       test/testcases/tst_pthread.c:38,145-309 restated: nthreads threads
+ *       (MPI_THREAD_MULTIPLE), each on its own file <prefix>.<id> over
+ *       MPI_COMM_SELF: a record variable ivar(time, X) NC_INT and a fixed
+ *       dvar(Y, X) NC_DOUBLE; records 0 and 2 of ivar with
+ *       ncmpi_put_vara_int[_all], dvar with ncmpi_put_var_double[_all],
+ *       sync, close; after a barrier of the threads each thread opens the
+ *       file of thread id+1, reads both records and dvar back and checks
+ *       them.  Values: ivar record r element i = id*1000003 + r*7919 + i,
+ *       dvar element i = id + i*0.5.  dev = 1: hipMalloc'ed buffers.
+ *       One JSON line per thread: the variables' offsets, recsize, errors.
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 #include <mpi.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -363,9 +376,13 @@ static void phases_print(const char *label, int calls)
  * got once with ncmpi_get_vara_int_all; per-call medians, plus the put loop,
  * the get loop and the close timed whole.  Every record's values differ
  * (record r holds v + r), and every element read back is checked. */
-static int mode_c1first(const char *path, MPI_Offset n, int nrec, int dev)
+static int mode_c1first(const char *path, MPI_Offset n, int nrec, int dev, int dbl)
 {
+    /* dbl: the user buffers are double (ncmpi_put/get_vara_double_all into
+     * the NC_INT variable, a cross-type conversion) */
+    const size_t ub = (size_t)n * (dbl ? 8 : 4);
     int *h = (int *)malloc((size_t)n * 4), *g = (int *)calloc((size_t)n, 4), ncid, dimid[2], varid, r, bad = 0;
+    double *hd = dbl ? (double *)malloc(ub) : NULL, *gd = dbl ? (double *)calloc((size_t)n, 8) : NULL;
     double *tp = (double *)calloc((size_t)nrec, sizeof(double)), *tg = (double *)calloc((size_t)nrec, sizeof(double));
     double put_loop, get_loop, t_close, t0, t_open, t_create;
     void *dh = NULL, *dg = NULL;
@@ -374,8 +391,8 @@ static int mode_c1first(const char *path, MPI_Offset n, int nrec, int dev)
     long long put_n[64] = {0}, first_n[64] = {0};
     for (i = 0; i < n; i++) h[i] = (int)((uint32_t)i * 2654435761u);
     if (dev) {
-        dh = to_dev(NULL, (size_t)n * 4);
-        dg = to_dev(NULL, (size_t)n * 4);
+        dh = to_dev(NULL, ub);
+        dg = to_dev(NULL, ub);
     }
     t_open = MPI_Wtime();
     CHECK(ncmpi_create(MPI_COMM_WORLD, path, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid));
@@ -390,7 +407,8 @@ static int mode_c1first(const char *path, MPI_Offset n, int nrec, int dev)
     put_loop = MPI_Wtime();
     for (r = 0; r < nrec; r++) {
         for (i = 0; i < n; i++) h[i] += 1;                   /* a new record's values */
-        if (dev && hipMemcpy(dh, h, (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess) { fprintf(stderr, "H2D failed\n"); exit(3); }
+        if (dbl) for (i = 0; i < n; i++) hd[i] = (double)h[i];
+        if (dev && hipMemcpy(dh, dbl ? (void *)hd : (void *)h, ub, hipMemcpyHostToDevice) != hipSuccess) { fprintf(stderr, "H2D failed\n"); exit(3); }
         start[0] = r;
         if (r == 1 && phases_on()) {                         /* phases of the calls after the first */
             const char *(*name)(int) = (const char *(*)(int))dlsym(RTLD_DEFAULT, "pncx_phase_name");
@@ -400,7 +418,8 @@ static int mode_c1first(const char *path, MPI_Offset n, int nrec, int dev)
             phases_reset();
         }
         t0 = MPI_Wtime();
-        CHECK(ncmpi_put_vara_int_all(ncid, varid, start, count, dev ? dh : (void *)h));
+        if (dbl) CHECK(ncmpi_put_vara_double_all(ncid, varid, start, count, dev ? dh : (void *)hd));
+        else CHECK(ncmpi_put_vara_int_all(ncid, varid, start, count, dev ? dh : (void *)h));
         tp[r] = MPI_Wtime() - t0;
     }
     put_loop = MPI_Wtime() - put_loop;
@@ -420,12 +439,14 @@ static int mode_c1first(const char *path, MPI_Offset n, int nrec, int dev)
         start[0] = r;
         if (r == 1 && phases_on()) phases_reset();
         t0 = MPI_Wtime();
-        CHECK(ncmpi_get_vara_int_all(ncid, varid, start, count, dev ? dg : (void *)g));
+        if (dbl) CHECK(ncmpi_get_vara_double_all(ncid, varid, start, count, dev ? dg : (void *)gd));
+        else CHECK(ncmpi_get_vara_int_all(ncid, varid, start, count, dev ? dg : (void *)g));
         tg[r] = MPI_Wtime() - t0;
         get_loop += tg[r];
         if (r == 0) get_first = tg[0];
-        if (dev) from_dev(g, dg, (size_t)n * 4);
-        for (i = 0; i < n && !bad; i++) bad = g[i] != h[i] + r + 1;
+        if (dev) from_dev(dbl ? (void *)gd : (void *)g, dg, ub);
+        if (dbl) for (i = 0; i < n && !bad; i++) bad = gd[i] != (double)(int)(h[i] + r + 1);
+        else for (i = 0; i < n && !bad; i++) bad = g[i] != h[i] + r + 1;
     }
     t0 = MPI_Wtime();
     CHECK(ncmpi_close(ncid));
@@ -459,7 +480,7 @@ static int mode_c1first(const char *path, MPI_Offset n, int nrec, int dev)
     }
     printf("}\n");
     if (dev) { hipFree(dh); hipFree(dg); }
-    free(h); free(g); free(tp); free(tg);
+    free(h); free(g); free(hd); free(gd); free(tp); free(tg);
     return nerrs != 0;
 }
 
@@ -882,16 +903,160 @@ static int mode_header(const char *path)
     return nerrs != 0;
 }
 
+/* ------------------------------------------------------------------ pthread */
+typedef struct {
+    const char *prefix;
+    int id, nthreads, coll, dev;
+    MPI_Offset nx, ny;
+    pthread_barrier_t *barr;
+    char out[512];
+    int errs;
+} pt_arg;
+
+#define TCHECK(call)                                                                                      \
+    do {                                                                                                  \
+        int _e = (call);                                                                                  \
+        if (_e != NC_NOERR) {                                                                             \
+            fprintf(stderr, "thread %d %s:%d: %s -> %d %s\n", a->id, __FILE__, __LINE__, #call, _e,          \
+                    ncmpi_strerror(_e));                                                                  \
+            a->errs++;                                                                                    \
+        }                                                                                                 \
+    } while (0)
+
+static int pt_ival(int id, int r, MPI_Offset i) { return (int)((uint32_t)id * 1000003u + (uint32_t)r * 7919u + (uint32_t)i); }
+static double pt_dval(int id, MPI_Offset i) { return (double)id + 0.5 * (double)i; }
+
+static void *pt_main(void *p)
+{
+    pt_arg *a = (pt_arg *)p;
+    const MPI_Offset nx = a->nx, ny = a->ny;
+    int *ib = (int *)malloc(sizeof(int) * (size_t)nx);
+    double *db = (double *)malloc(sizeof(double) * (size_t)(nx * ny));
+    void *dib = NULL, *ddb = NULL;
+    char fn[1024];
+    int ncid, dimid[2], varid[2], r, id = a->id;
+    MPI_Offset start[2], count[2], i, ioff = -1, doff = -1, recsize = -1;
+    MPI_Info info;
+    snprintf(fn, sizeof fn, "%s.%d", a->prefix, id);
+    MPI_Info_create(&info);
+    MPI_Info_set(info, "nc_var_align_size", "1");
+    TCHECK(ncmpi_create(MPI_COMM_SELF, fn, NC_CLOBBER, info, &ncid));
+    MPI_Info_free(&info);
+    TCHECK(ncmpi_def_dim(ncid, "time", NC_UNLIMITED, &dimid[0]));
+    TCHECK(ncmpi_def_dim(ncid, "X", nx, &dimid[1]));
+    TCHECK(ncmpi_def_var(ncid, "ivar", NC_INT, 2, dimid, &varid[0]));
+    TCHECK(ncmpi_def_dim(ncid, "Y", ny, &dimid[0]));
+    TCHECK(ncmpi_def_var(ncid, "dvar", NC_DOUBLE, 2, dimid, &varid[1]));
+    TCHECK(ncmpi_enddef(ncid));
+    if (!a->coll) TCHECK(ncmpi_begin_indep_data(ncid));
+    if (a->dev) { dib = to_dev(NULL, sizeof(int) * (size_t)nx); ddb = to_dev(NULL, sizeof(double) * (size_t)(nx * ny)); }
+    for (r = 0; r <= 2; r += 2) {                         /* records 0 and 2 (tst_pthread.c:186-207) */
+        for (i = 0; i < nx; i++) ib[i] = pt_ival(id, r, i);
+        if (a->dev && hipMemcpy(dib, ib, sizeof(int) * (size_t)nx, hipMemcpyHostToDevice) != hipSuccess) a->errs++;
+        start[0] = r; start[1] = 0; count[0] = 1; count[1] = nx;
+        if (a->coll) TCHECK(ncmpi_put_vara_int_all(ncid, varid[0], start, count, a->dev ? dib : (void *)ib));
+        else TCHECK(ncmpi_put_vara_int(ncid, varid[0], start, count, a->dev ? dib : (void *)ib));
+    }
+    for (i = 0; i < nx * ny; i++) db[i] = pt_dval(id, i);
+    if (a->dev && hipMemcpy(ddb, db, sizeof(double) * (size_t)(nx * ny), hipMemcpyHostToDevice) != hipSuccess) a->errs++;
+    if (a->coll) TCHECK(ncmpi_put_var_double_all(ncid, varid[1], a->dev ? ddb : (void *)db));
+    else TCHECK(ncmpi_put_var_double(ncid, varid[1], a->dev ? ddb : (void *)db));
+    TCHECK(ncmpi_sync(ncid));
+    TCHECK(ncmpi_inq_varoffset(ncid, varid[0], &ioff));
+    TCHECK(ncmpi_inq_varoffset(ncid, varid[1], &doff));
+    TCHECK(ncmpi_inq_recsize(ncid, &recsize));
+    TCHECK(ncmpi_close(ncid));
+    pthread_barrier_wait(a->barr);                        /* every file is written (tst_pthread.c:226) */
+    id = (id + 1) % a->nthreads;                          /* another thread's file (:232-234) */
+    snprintf(fn, sizeof fn, "%s.%d", a->prefix, id);
+    TCHECK(ncmpi_open(MPI_COMM_SELF, fn, NC_NOWRITE, MPI_INFO_NULL, &ncid));
+    if (!a->coll) TCHECK(ncmpi_begin_indep_data(ncid));
+    TCHECK(ncmpi_inq_varid(ncid, "ivar", &varid[0]));
+    TCHECK(ncmpi_inq_varid(ncid, "dvar", &varid[1]));
+    for (r = 0; r <= 2; r += 2) {
+        for (i = 0; i < nx; i++) ib[i] = -1;
+        if (a->dev) (void)hipMemset(dib, 0xff, sizeof(int) * (size_t)nx);
+        start[0] = r; start[1] = 0; count[0] = 1; count[1] = nx;
+        if (a->coll) TCHECK(ncmpi_get_vara_int_all(ncid, varid[0], start, count, a->dev ? dib : (void *)ib));
+        else TCHECK(ncmpi_get_vara_int(ncid, varid[0], start, count, a->dev ? dib : (void *)ib));
+        if (a->dev) from_dev(ib, dib, sizeof(int) * (size_t)nx);
+        for (i = 0; i < nx; i++)
+            if (ib[i] != pt_ival(id, r, i)) {
+                fprintf(stderr, "thread %d: file %d record %d element %lld: %d != %d\n", a->id, id, r, (long long)i,
+                        ib[i], pt_ival(id, r, i));
+                a->errs++;
+                break;
+            }
+    }
+    for (i = 0; i < nx * ny; i++) db[i] = -1.0;
+    if (a->dev) (void)hipMemset(ddb, 0xff, sizeof(double) * (size_t)(nx * ny));
+    if (a->coll) TCHECK(ncmpi_get_var_double_all(ncid, varid[1], a->dev ? ddb : (void *)db));
+    else TCHECK(ncmpi_get_var_double(ncid, varid[1], a->dev ? ddb : (void *)db));
+    if (a->dev) from_dev(db, ddb, sizeof(double) * (size_t)(nx * ny));
+    for (i = 0; i < nx * ny; i++)
+        if (db[i] != pt_dval(id, i)) {
+            fprintf(stderr, "thread %d: file %d dvar element %lld: %g != %g\n", a->id, id, (long long)i, db[i],
+                    pt_dval(id, i));
+            a->errs++;
+            break;
+        }
+    TCHECK(ncmpi_close(ncid));
+    if (a->dev) { hipFree(dib); hipFree(ddb); }
+    free(ib);
+    free(db);
+    snprintf(a->out, sizeof a->out,
+             "{\"mode\": \"pthread\", \"thread\": %d, \"file\": \"%s.%d\", \"ivar_off\": %lld, \"dvar_off\": %lld, "
+             "\"recsize\": %lld, \"errors\": %d}", a->id, a->prefix, a->id, (long long)ioff, (long long)doff,
+             (long long)recsize, a->errs);
+    return NULL;
+}
+
+static int mode_pthread(const char *prefix, int nthreads, MPI_Offset nx, MPI_Offset ny, int coll, int dev, int provided)
+{
+    pt_arg *args = (pt_arg *)calloc((size_t)nthreads, sizeof(pt_arg));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    pthread_barrier_t barr;
+    int t, errs = 0, ncid;
+    if (provided < MPI_THREAD_MULTIPLE) {
+        fprintf(stderr, "MPI_Init_thread gave thread level %d < MPI_THREAD_MULTIPLE\n", provided);
+        return 1;
+    }
+    pthread_barrier_init(&barr, NULL, (unsigned)nthreads);
+    for (t = 0; t < nthreads; t++) {
+        args[t].prefix = prefix; args[t].id = t; args[t].nthreads = nthreads; args[t].coll = coll;
+        args[t].dev = dev; args[t].nx = nx; args[t].ny = ny; args[t].barr = &barr;
+        if (pthread_create(&th[t], NULL, pt_main, &args[t]) != 0) { fprintf(stderr, "pthread_create\n"); return 1; }
+    }
+    for (t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        errs += args[t].errs;
+        printf("%s\n", args[t].out);
+    }
+    pthread_barrier_destroy(&barr);
+    for (t = 0; t < nthreads; t++) {                      /* every file opens again (tst_pthread.c:349-358) */
+        char fn[1024];
+        snprintf(fn, sizeof fn, "%s.%d", prefix, t);
+        CHECK(ncmpi_open(MPI_COMM_SELF, fn, NC_NOWRITE, MPI_INFO_NULL, &ncid));
+        CHECK(ncmpi_close(ncid));
+    }
+    printf("{\"mode\": \"pthread\", \"threads\": %d, \"errors\": %d}\n", nthreads, errs + nerrs);
+    free(args);
+    free(th);
+    return errs + nerrs != 0;
+}
+
 int main(int argc, char **argv)
 {
-    int rc = 2;
-    MPI_Init(&argc, &argv);
+    int rc = 2, provided = 0;
+    if (argc >= 2 && strcmp(argv[1], "pthread") == 0) MPI_Init_thread(&argc, &argv, MPI_THREAD_MULTIPLE, &provided);
+    else MPI_Init(&argc, &argv);
     if (argc >= 5 && strcmp(argv[1], "c1") == 0)
         rc = mode_c1(argv[2], argv[3], atoll(argv[4]), argc >= 6 ? atoi(argv[5]) : 0);
     else if (argc >= 6 && strcmp(argv[1], "c1bench") == 0)
         rc = mode_c1bench(argv[2], atoll(argv[3]), atoi(argv[4]), atoi(argv[5]));
     else if (argc >= 6 && strcmp(argv[1], "c1first") == 0)
-        rc = mode_c1first(argv[2], atoll(argv[3]), atoi(argv[4]), atoi(argv[5]));
+        rc = mode_c1first(argv[2], atoll(argv[3]), atoi(argv[4]), atoi(argv[5]),
+                          argc >= 7 && strcmp(argv[6], "double") == 0);
     else if (argc >= 8 && strcmp(argv[1], "c1ab") == 0)
         rc = mode_c1ab(argv[2], atoll(argv[3]), atoi(argv[4]), argv[5], atoll(argv[6]), atoll(argv[7]),
                        argc >= 9 ? atoi(argv[8]) : 0);
@@ -907,6 +1072,9 @@ int main(int argc, char **argv)
     else if (argc >= 3 && strcmp(argv[1], "errors") == 0) rc = mode_errors(argv[2]);
     else if (argc >= 3 && strcmp(argv[1], "header") == 0) rc = mode_header(argv[2]);
     else if (argc >= 4 && strcmp(argv[1], "flexdev") == 0) rc = mode_flexdev(argv[2], atoi(argv[3]));
+    else if (argc >= 7 && strcmp(argv[1], "pthread") == 0)
+        rc = mode_pthread(argv[2], atoi(argv[3]), atoll(argv[4]), atoll(argv[5]), atoi(argv[6]),
+                          argc >= 8 ? atoi(argv[7]) : 0, provided);
     else fprintf(stderr, "usage: see the header of api_check.c\n");
     MPI_Finalize();
     return rc;

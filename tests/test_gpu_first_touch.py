@@ -135,3 +135,44 @@ def test_appends_same_with_and_without_first_touch_paths(gpu, shm_dir, knob, xt,
     for r in (2, 4):                                 # never written: the holes read as zeros
         off = v["begin"] + r * xs * n
         assert raw[off:off + xs * n] == b"\0" * (xs * n)
+
+
+@pytest.mark.parametrize("where", ["host", "dev"])
+def test_failed_append_cuts_the_file_back(gpu, shm_dir, knob, where):
+    """an appending put that grows the file (grow_for_put) and then fails
+    before writing anything (PNCX_FAULT=1, test-only injection right after
+    the grow) leaves the file at its size before the put -- what the
+    reference's convert-then-pwrite leaves (ncmpio_getput.m4:186-214) --
+    and the next put appends normally"""
+    torch = gpu
+    n = (1 << 18) + 7
+    path = os.path.join(shm_dir, "fault.nc")
+    err, ncid = N.create(path, N.NC_64BIT_DATA)
+    assert err == 0
+    N.def_dim(ncid, "t", N.NC_UNLIMITED)
+    N.def_dim(ncid, "x", n)
+    N.def_var(ncid, "r", T.NC_INT, [0, 1])
+    assert N.enddef(ncid) == 0
+    vals = np.arange(n, dtype=np.int32) * 3 - 7
+
+    def put(r):
+        if where == "dev":
+            return N.put_var_dev(ncid, 0, torch.from_numpy(vals + r).cuda(), [r, 0], [1, n])
+        return N.put_var(ncid, 0, vals + r, [r, 0], [1, n], itype=T.ITYPE_INT)
+
+    assert put(0) == 0
+    size0 = os.path.getsize(path)
+    knob("FAULT", 1)
+    assert put(1) == N.NC_EWRITE
+    assert os.path.getsize(path) == size0, "the failed put left a grown tail"
+    knob("FAULT", 0)
+    assert put(1) == 0
+    assert N.close(ncid) == 0
+    raw = open(path, "rb").read()
+    h = cdfparse.parse_cdf(raw)
+    v = h["vars"][0]
+    assert h["numrecs"] == 2 and len(raw) == v["begin"] + 2 * 4 * n
+    ora = OracleConv()
+    for r in (0, 1):
+        exp, st = ora.putn(5, T.NC_INT, vals + r, T.ITYPE_INT, T.fill_bytes(T.NC_INT))
+        assert raw[v["begin"] + r * 4 * n:v["begin"] + (r + 1) * 4 * n] == exp, r

@@ -13,6 +13,7 @@ int pncxrt_device_count(void) { return 0; }
 int pncxrt_set_device(int dev) { (void)dev; return NODEV; }
 int pncxrt_get_device(void) { return 0; }
 int pncxrt_load_swap_code(void) { return NODEV; }
+int pncxk_load_xtype(int x) { (void)x; return NODEV; }
 int pncxrt_malloc(void **p, size_t n) { (void)p; (void)n; return NODEV; }
 int pncxrt_free(void *p) { (void)p; return 0; }
 int pncxrt_host_alloc(void **p, size_t n) { (void)p; (void)n; return NODEV; }
