@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     order = sys.argv[1] if len(sys.argv) > 1 else "spgd"
     t0 = time.perf_counter()
-    lib = ctypes.CDLL(os.path.join(ROOT, "pnetcdf_amd", "lib", "libpncx.so"))
+    lib = ctypes.CDLL(os.environ.get("PNCX_LIB_PATH", os.path.join(ROOT, "pnetcdf_amd", "lib", "libpncx.so")))
     hip = ctypes.CDLL("libamdhip64.so")
     t_load = time.perf_counter() - t0
     t0 = time.perf_counter()
