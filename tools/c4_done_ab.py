@@ -1,14 +1,17 @@
 """C4's synchronous call (pncx_dev_batch, swaps only: no statuses to bring
-back) waiting on an event after the batch kernel (PNCX_DONE_EVENT, default)
-against the completion kernel and its host-mapped flag (0), in one process,
-knob order A B B A per round; wall time of --steps calls, as bench.py times
-the call.  Both settings' outputs are checked (bench.py C4Batch.check).
+back) waiting on a completion event against the completion kernel and its
+host-mapped flag (0, the default), in one process, knob order A B B A per
+round; wall time of --steps calls, as bench.py times the call.  Both
+settings' outputs are checked (bench.py C4Batch.check).
 
     python tools/c4_done_ab.py [--rounds 6] [--steps 100]
 
-Ran once (profiles/r05w_done_ab.txt): the event was slower (0.2669 against
-0.2634 ms per call) and was removed with its knob; the script needs the
-knob back to run again.
+Round 5 (profiles/r05w_done_ab.txt): an event RECORDED after the batch
+kernel (a marker packet) and polled with hipEventQuery was slower (0.2669
+against 0.2634 ms per call) and was removed.  Round 6: PNCX_DONE_EVENT=1 is
+an event stamped by the batch kernel's own dispatch (hipExtLaunchKernel's
+stop event, no extra packet), polled the same way: also slower (0.2625
+against 0.2609 ms, profiles/r06h_done_ab.txt), removed with its knob.
 """
 import argparse
 import ctypes
