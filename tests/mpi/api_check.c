@@ -65,6 +65,10 @@
  *       them.  Values: ivar record r element i = id*1000003 + r*7919 + i,
  *       dvar element i = id + i*0.5.  dev = 1: hipMalloc'ed buffers.
  *       One JSON line per thread: the variables' offsets, recsize, errors.
+ *   api_check pthreadhdr <prefix> <nthreads> <iters>
+ *       define-mode only, no GPU: each thread creates / defines / closes /
+ *       reopens / inquires / closes its own file iters times; no file may
+ *       stay open at the end (the ncid table under threads).
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -1011,6 +1015,67 @@ static void *pt_main(void *p)
     return NULL;
 }
 
+/* define-mode traffic from many threads at once (no data call, so no GPU
+ * needed): each thread creates, defines, ends define mode, closes, reopens,
+ * looks its variable up and closes its own file, iters times; the ncid
+ * table (pnc_dispatch.c) hands out and retires ids under its mutex.  At the
+ * end no file may be left open. */
+typedef struct { const char *prefix; int id, iters, errs; } ph_arg;
+
+static void *ph_main(void *p)
+{
+    ph_arg *a = (ph_arg *)p;
+    char fn[1024];
+    int k;
+    snprintf(fn, sizeof fn, "%s.%d", a->prefix, a->id);
+    for (k = 0; k < a->iters; k++) {
+        int ncid = -1, ncid2 = -1, d[2], v, v2 = -1, e;
+        MPI_Offset len = -1;
+        e = ncmpi_create(MPI_COMM_SELF, fn, NC_CLOBBER | NC_64BIT_DATA, MPI_INFO_NULL, &ncid);
+        if (!e) e = ncmpi_def_dim(ncid, "time", NC_UNLIMITED, &d[0]);
+        if (!e) e = ncmpi_def_dim(ncid, "x", 16 + a->id, &d[1]);
+        if (!e) e = ncmpi_def_var(ncid, "v", NC_INT, 2, d, &v);
+        if (!e) e = ncmpi_enddef(ncid);
+        if (!e) e = ncmpi_close(ncid);
+        if (!e) e = ncmpi_open(MPI_COMM_SELF, fn, NC_NOWRITE, MPI_INFO_NULL, &ncid2);
+        if (!e) e = ncmpi_inq_varid(ncid2, "v", &v2);
+        if (!e) e = ncmpi_inq_dimlen(ncid2, 1, &len);
+        if (!e && (v2 != v || len != 16 + a->id)) e = NC_EINTERNAL;
+        if (!e) e = ncmpi_close(ncid2);
+        if (e) {
+            fprintf(stderr, "thread %d iteration %d: %d %s\n", a->id, k, e, ncmpi_strerror(e));
+            a->errs++;
+            break;
+        }
+    }
+    return NULL;
+}
+
+static int mode_pthread_hdr(const char *prefix, int nthreads, int iters, int provided)
+{
+    ph_arg *args = (ph_arg *)calloc((size_t)nthreads, sizeof(ph_arg));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    int t, errs = 0, nopen = -1;
+    if (provided < MPI_THREAD_MULTIPLE) {
+        fprintf(stderr, "MPI_Init_thread gave thread level %d < MPI_THREAD_MULTIPLE\n", provided);
+        return 1;
+    }
+    for (t = 0; t < nthreads; t++) {
+        args[t].prefix = prefix; args[t].id = t; args[t].iters = iters;
+        if (pthread_create(&th[t], NULL, ph_main, &args[t]) != 0) { fprintf(stderr, "pthread_create\n"); return 1; }
+    }
+    for (t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        errs += args[t].errs;
+    }
+    CHECK(ncmpi_inq_files_opened(&nopen, NULL));
+    printf("{\"mode\": \"pthreadhdr\", \"threads\": %d, \"iters\": %d, \"files_open\": %d, \"errors\": %d}\n",
+           nthreads, iters, nopen, errs + nerrs);
+    free(args);
+    free(th);
+    return errs + nerrs != 0 || nopen != 0;
+}
+
 static int mode_pthread(const char *prefix, int nthreads, MPI_Offset nx, MPI_Offset ny, int coll, int dev, int provided)
 {
     pt_arg *args = (pt_arg *)calloc((size_t)nthreads, sizeof(pt_arg));
@@ -1048,7 +1113,7 @@ static int mode_pthread(const char *prefix, int nthreads, MPI_Offset nx, MPI_Off
 int main(int argc, char **argv)
 {
     int rc = 2, provided = 0;
-    if (argc >= 2 && strcmp(argv[1], "pthread") == 0) MPI_Init_thread(&argc, &argv, MPI_THREAD_MULTIPLE, &provided);
+    if (argc >= 2 && strncmp(argv[1], "pthread", 7) == 0) MPI_Init_thread(&argc, &argv, MPI_THREAD_MULTIPLE, &provided);
     else MPI_Init(&argc, &argv);
     if (argc >= 5 && strcmp(argv[1], "c1") == 0)
         rc = mode_c1(argv[2], argv[3], atoll(argv[4]), argc >= 6 ? atoi(argv[5]) : 0);
@@ -1072,6 +1137,8 @@ int main(int argc, char **argv)
     else if (argc >= 3 && strcmp(argv[1], "errors") == 0) rc = mode_errors(argv[2]);
     else if (argc >= 3 && strcmp(argv[1], "header") == 0) rc = mode_header(argv[2]);
     else if (argc >= 4 && strcmp(argv[1], "flexdev") == 0) rc = mode_flexdev(argv[2], atoi(argv[3]));
+    else if (argc >= 5 && strcmp(argv[1], "pthreadhdr") == 0)
+        rc = mode_pthread_hdr(argv[2], atoi(argv[3]), atoi(argv[4]), provided);
     else if (argc >= 7 && strcmp(argv[1], "pthread") == 0)
         rc = mode_pthread(argv[2], atoi(argv[3]), atoll(argv[4]), atoll(argv[5]), atoi(argv[6]),
                           argc >= 8 ? atoi(argv[7]) : 0, provided);

@@ -155,3 +155,18 @@ def test_ncmpii_need_convert_with_mpi_datatypes(tmp_path):
     capi.run([capi.exe("ncmpii_check"), "run", cp, op])
     got = [st for st, _ in capi.read_results(op)]
     assert got == exp
+
+
+def test_ncid_table_under_threads(tmp_path):
+    """32 threads of one process create, define, close, reopen, inquire
+    and close their own files 300 times each through the public API
+    (api_check pthreadhdr; define mode only, so no GPU).  The dispatcher's
+    ncid table is guarded by a mutex as the reference's is under
+    PNETCDF_THREAD_SAFE (src/dispatchers/file.c:30-33,621-703); without it
+    this program crashes or reports NC_EBADID within a few iterations.  No
+    error, and no file left open.  The data-path restatement of
+    tst_pthread.c runs on the GPU (tests/test_gpu_pthread.py)."""
+    import json
+    r = capi.run([capi.exe("api_check"), "pthreadhdr", str(tmp_path / "thr.nc"), "32", "300"], timeout=120)
+    (line,) = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert line["errors"] == 0 and line["files_open"] == 0 and line["threads"] == 32
