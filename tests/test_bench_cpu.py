@@ -152,3 +152,26 @@ def test_c1_first_order_interleaves_and_brackets():
     assert runs[len(order) - 2]["put_vs_reference"] == 2.0
     assert all(r["get_vs_reference"] == 4.0 and r["put_loop_vs_reference"] == 2.0
                for k, r in zip(order, runs) if k != "ref")
+
+
+def test_bench_line_compact_at_eight_ranks():
+    """The N = 8 line (no C1; per-rank kernel times, the rank report and
+    the gather leg added) also stays under the limit and keeps them."""
+    bench, full = _canned_full()
+    del full["workloads"]["c1"]
+    full["n_gpus"] = 8
+    for w in full["workloads"].values():
+        w["kernel_ms_per_rank"] = [0.2512] * 8
+        w["n_gpus"] = 8
+    full["ranks"] = {"backend": "rccl", "world_size": 8, "local_device_of_rank0": "0000:05:00",
+                     "distinct_devices": True, "pci_of_ranks": ["0000:%02x:00" % (5 + 16 * i) for i in range(8)],
+                     "rccl_world_size": 8, "kernel_ms_per_rank": [10.0671] * 8}
+    full["gather"] = {"collective": "gather into rank 0 (RCCL over xGMI)", "bytes_per_rank": 1 << 35,
+                      "bytes_into_rank0": 7 << 35, "chunk_bytes_per_rank": 1 << 31, "chunks": 16, "ms": 400.0,
+                      "GBps_into_rank0": 600.0, "checksums_ok": True, "via_xgmi": True, "pcie_ceiling_GBps": 57.5,
+                      "note": "x" * 100}
+    line = bench.compact_line(full)
+    s = json.dumps(line)
+    assert len(s) < bench.LINE_MAX_CHARS, len(s)
+    assert line["ranks"]["distinct_devices"] and line["gather"]["checksums_ok"]
+    assert all(len(w["kernel_ms_per_rank"]) == 8 for w in line["workloads"].values())
