@@ -1,4 +1,5 @@
 # C4 synchronous completion: kernel-stamped event (PNCX_DONE_EVENT=1) against
+# (historical: the knob it A/Bs was removed after the run; kept as the record of how its profiles/ file was made)
 # the completion block (0); then the batch parity tests with the event on
 set -o pipefail
 mkdir -p gpurun_out

@@ -1,4 +1,5 @@
 # Transpose tile order: the shipped order (skew 8 put / 32 get for the
+# (historical: the knob it A/Bs was removed after the run; kept as the record of how its profiles/ file was made)
 # x254 stride, row-major merged, diagonal 2-D) against "spread"
 # (PNCX_XPOSE_ORDER=2000: p tiles run (tp * ~tp/64) mod tp, so the tiles
 # resident at once cover the packed address bits below the column stride);
