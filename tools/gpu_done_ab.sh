@@ -1,6 +1,6 @@
 # C4 synchronous completion: kernel-stamped event (PNCX_DONE_EVENT=1) against
-# (historical: the knob it A/Bs was removed after the run; kept as the record of how its profiles/ file was made)
 # the completion block (0); then the batch parity tests with the event on
+# (historical: the knob it A/Bs was removed after the run; kept as the record of how its profiles/ file was made)
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python3 tools/c4_done_ab.py --rounds 6 --steps 100 > gpurun_out/r06h_done_ab.txt 2>&1 || exit 1

@@ -1,7 +1,7 @@
 # Cache-pull helpers (PNCX_PULL) on the C1 first-touch put: in-process A/B
-# (historical: the knob it A/Bs was removed after the run; kept as the record of how its profiles/ file was made)
 # (api_check c1ab alternates the knob record by record, A B B A ...) and
 # whole processes with per-phase times (api_check c1first, PNCX_PHASES=1)
+# (historical: the knob it A/Bs was removed after the run; kept as the record of how its profiles/ file was made)
 set -o pipefail
 out=${OUT:-gpurun_out/r06d_pull_ab.txt}
 mkdir -p gpurun_out
