@@ -29,9 +29,46 @@ STORE = re.compile(r"^\s*(global|buffer|flat)_store_dwordx([34])\s+(.*?)\s*//")
 VREG = re.compile(r"v\[(\d+):(\d+)\]|\bv(\d+)\b")
 
 
+BUNDLER = "/opt/rocm/lib/llvm/bin/clang-offload-bundler"
+CMAGIC = b"CCOB"           # a compressed offload bundle (hipcc --offload-compress, the library's default)
+
+
+def _compressed_code_objects(data):
+    """The gfx950 code objects of the compressed bundles (CCOB version 2/3:
+    magic, version, method, total size, uncompressed size, hash; the sizes
+    are 32-bit in version 2, 64-bit in 3), unbundled and decompressed by
+    clang-offload-bundler."""
+    import tempfile
+    out, pos = [], 0
+    with tempfile.TemporaryDirectory() as td:
+        while True:
+            i = data.find(CMAGIC, pos)
+            if i < 0:
+                return out
+            pos = i + 4
+            ver, method = struct.unpack_from("<HH", data, i + 4)
+            if ver not in (2, 3):
+                continue
+            total = struct.unpack_from("<Q" if ver == 3 else "<I", data, i + 8)[0]
+            if total <= 24 or i + total > len(data):
+                continue
+            src, dst = os.path.join(td, "b.bin"), os.path.join(td, "b.co")
+            with open(src, "wb") as f:
+                f.write(data[i:i + total])
+            r = subprocess.run([BUNDLER, "--unbundle", "--type=o", "--input=" + src,
+                                "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + dst],
+                               capture_output=True, timeout=120)
+            if r.returncode == 0 and os.path.getsize(dst) > 0:
+                out.append(open(dst, "rb").read())
+            pos = i + total
+
+
 def code_objects(path):
-    """The gfx950 ELF code objects of every offload bundle in the library."""
+    """The gfx950 ELF code objects of every offload bundle in the library
+    (plain bundles read in place, compressed ones through the bundler)."""
     data = open(path, "rb").read()
+    if data.find(MAGIC) < 0 and data.find(CMAGIC) >= 0:
+        return _compressed_code_objects(data)
     out, pos = [], 0
     while True:
         i = data.find(MAGIC, pos)
