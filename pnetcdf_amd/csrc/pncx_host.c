@@ -312,7 +312,16 @@ static int launch_op(const op_t *op, const void *src, void *dst, long long n, in
     }
 }
 
-static int have_device(void) { return pncxrt_device_count() > 0; }
+/* a device count above zero stays so for the process: cached, so that every
+ * call does not ask the runtime again */
+static int g_have_dev;
+static int have_device(void)
+{
+    if (__atomic_load_n(&g_have_dev, __ATOMIC_RELAXED)) return 1;
+    if (pncxrt_device_count() <= 0) return 0;
+    __atomic_store_n(&g_have_dev, 1, __ATOMIC_RELAXED);
+    return 1;
+}
 
 /* ------------------------------------------------------------------------ */
 /* device-resident entry points                                              */
