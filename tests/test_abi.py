@@ -131,6 +131,13 @@ def test_no_cpu_fallback_without_gpu(built):
     rc = L.pncx_putn(5, 42, ctypes.c_void_p(xb.ctypes.data), ctypes.c_void_p(buf.ctypes.data),
                      ctypes.c_longlong(16), T.ITYPE_INT, None)
     assert rc == T.NC_EBADTYPE
+    # the enddef preload (round 6): nothing to load without a device; the
+    # pending mask is the request minus NC_CHAR
+    mask = (1 << T.NC_INT) | (1 << T.NC_DOUBLE) | (1 << T.NC_CHAR)
+    assert L.pncx_preload_xtypes(0, mask) == T.PNCX_EDEVICE
+    L.pncx_preload_pending.restype = ctypes.c_uint
+    assert L.pncx_preload_pending(0, mask) == (1 << T.NC_INT) | (1 << T.NC_DOUBLE)
+    assert L.pncx_preload_pending(-1, mask) == 0
 
 
 def test_ncmpii_in_swapn_aborts_without_gpu(built):
