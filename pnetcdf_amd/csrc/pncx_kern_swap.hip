@@ -465,8 +465,21 @@ __global__ __launch_bounds__(256) void k_batch_done(const int *dstat, int n, int
     if (threadIdx.x == 0) __hip_atomic_store(hdone, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// A batch with no statuses to bring back (swaps and copies only) has
+// nothing for a system-scope release to order before the flag -- the class
+// kernels' stores were released at their own end, before this kernel
+// started -- so one wave stores the flag relaxed: 0.7-0.8 us less per
+// synchronous call (C4 0.2570 -> 0.2562 ms through bench.py's loop, a
+// trivial call 10.0-11.5 -> 9.4-10.9 us from C; profiles/r06l_done_fence_ab.txt)
+__global__ __launch_bounds__(64) void k_batch_done_flag(int *hdone, int seq) {
+    if (threadIdx.x == 0) __hip_atomic_store(hdone, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 extern "C" int pncxk_batch_done(const int *dstat, int n, int *hstat, int *hdone, int seq, void *stream) {
-    hipLaunchKernelGGL(k_batch_done, dim3(1), dim3(256), 0, (hipStream_t)stream, dstat, n, hstat, hdone, seq);
+    if (n == 0)
+        hipLaunchKernelGGL(k_batch_done_flag, dim3(1), dim3(64), 0, (hipStream_t)stream, hdone, seq);
+    else
+        hipLaunchKernelGGL(k_batch_done, dim3(1), dim3(256), 0, (hipStream_t)stream, dstat, n, hstat, hdone, seq);
     return hipGetLastError() == hipSuccess ? 0 : PNCX_EDEVICE;
 }
 

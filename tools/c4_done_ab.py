@@ -29,6 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--knob", default="DONE_FENCE", help="the 0/1 knob to alternate")
     a = ap.parse_args()
     import torch
     import bench
@@ -42,7 +43,7 @@ def main():
     torch.cuda.synchronize()
     for r in range(a.rounds):
         for k in (1, 0, 0, 1):
-            pncx.knob_set("DONE_EVENT", k)
+            pncx.knob_set(a.knob, k)
             for _ in range(5):
                 wl.launch()
             torch.cuda.synchronize()
@@ -52,11 +53,11 @@ def main():
             torch.cuda.synchronize()
             res[k].append((time.perf_counter() - t0) * 1e3 / a.steps)
             assert wl.check(), f"DONE_EVENT={k}: wrong output"
-    pncx.knob_set("DONE_EVENT", -1)
+    pncx.knob_set(a.knob, -1)
     moved = 256 * (1 << 20) * 6
     for k, v in res.items():
         med = statistics.median(v)
-        print(json.dumps({"done_event": k, "call_ms_median": round(med, 4), "call_ms_min": round(min(v), 4),
+        print(json.dumps({a.knob.lower(): k, "call_ms_median": round(med, 4), "call_ms_min": round(min(v), 4),
                           "frac_of_8TBs": round(moved / (med * 1e-3) / 8e12, 4), "samples": len(v)}), flush=True)
 
 
