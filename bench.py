@@ -698,6 +698,8 @@ def c1_first_touch(nrec=32, n=1 << 20, cpu=True, reps=2):
         lib.orc_c1_first_sequence.restype = ctypes.c_int
         if rec_offset[0] is None:               # the library's header length for this variable
             rec_offset[0] = lib_run("host_1_io_thread", probe=True).get("rec_offset")
+        if rec_offset[0] is None:
+            return {"check_ok": False, "error": "no record offset (the library's probe run failed)"}
         o = (ctypes.c_double * 6)()
         rc = lib.orc_c1_first_sequence(path.encode(), rec_offset[0], n, nrec, o)
         return {"check_ok": rc == 0, "error": rc} if rc else {
