@@ -158,9 +158,10 @@ def test_read_only_open_leaves_the_device_alone(mode, expect):
     assert err == 0
     N.def_dim(ncid, "x", 4)
     assert N.enddef(ncid) == 0 and N.close(ncid) == 0
+    env = dict(os.environ, PNCX_WARM="1")       # the control needs the warm-up on, whatever the suite runs with
     try:
         r = subprocess.run([sys.executable, "-c", RO_OPEN.format(root=ROOT, path=path, mode=mode)],
-                           capture_output=True, text=True, timeout=120)
+                           capture_output=True, text=True, timeout=120, env=env)
         assert r.returncode == 0, r.stderr[-2000:]
         assert f"KFD {expect}" in r.stdout, r.stdout
     finally:
