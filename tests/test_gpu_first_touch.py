@@ -145,7 +145,10 @@ def test_failed_append_cuts_the_file_back(gpu, shm_dir, knob, where):
     reference's convert-then-pwrite leaves (ncmpio_getput.m4:186-214) --
     and the next put appends normally"""
     torch = gpu
-    n = (1 << 18) + 7
+    # the device put grows the file only on its one-slot path (the record
+    # within one staging slot, PNCX_STAGE_MB, and at least 1 MiB)
+    slot_mb = int(os.environ.get("PNCX_STAGE_MB", "32") or 32)
+    n = (1 << 18) + 7 if slot_mb > 1 or slot_mb <= 0 else 1 << 18
     path = os.path.join(shm_dir, "fault.nc")
     err, ncid = N.create(path, N.NC_64BIT_DATA)
     assert err == 0
@@ -160,6 +163,7 @@ def test_failed_append_cuts_the_file_back(gpu, shm_dir, knob, where):
             return N.put_var_dev(ncid, 0, torch.from_numpy(vals + r).cuda(), [r, 0], [1, n])
         return N.put_var(ncid, 0, vals + r, [r, 0], [1, n], itype=T.ITYPE_INT)
 
+    knob("GROW", 1)                             # whatever the suite runs with
     assert put(0) == 0
     size0 = os.path.getsize(path)
     knob("FAULT", 1)
