@@ -171,16 +171,22 @@ static int do_range(int fd, int write, const pio_run *runs, size_t n, long long 
     return err;
 }
 
+/* read once per process; every thread sees g_page set before the mode
+ * (a thread that found the mode set with g_page still 0 would divide by it) */
+static int g_mmap_mode;
+static pthread_once_t g_mmap_once = PTHREAD_ONCE_INIT;
+static void mmap_mode_init(void)
+{
+    const char *e = getenv("PNCX_IO_MMAP");
+    g_page = sysconf(_SC_PAGESIZE);
+    if (g_page <= 0) g_page = 4096;
+    g_mmap_mode = e ? atoi(e) != 0 : 1;
+}
+
 static int mmap_mode(void)
 {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("PNCX_IO_MMAP");
-        v = e ? atoi(e) != 0 : 1;
-        g_page = sysconf(_SC_PAGESIZE);
-        if (g_page <= 0) g_page = 4096;
-    }
-    return v;
+    pthread_once(&g_mmap_once, mmap_mode_init);
+    return g_mmap_mode;
 }
 
 /* Write job through mappings?  Large runs (>= MMAP_MIN) are each mapped;

@@ -1,0 +1,44 @@
+"""Host C code under ThreadSanitizer, on CPU (the
+library's shared state across threads).  tools/tsan/run.sh builds the file
+layer, the I/O pool and the host driver against a synchronous CPU stand-in
+for the device (tools/tsan/cpudev_stub.c, a test harness that is never part
+of the library) and runs tools/tsan/threads.c: six threads each create,
+write (NC_BYTE, NC_CHAR, NC_INT from host and "device" buffers, NC_DOUBLE;
+blocking and nonblocking), read back and reopen their own files, the shape
+of the reference's test/testcases/tst_pthread.c, while a seventh churns the
+file table.  Any data race report fails the run; the stand-in's launch
+counts show the device paths (staging, piece events, batch completion) ran.
+
+Round 6 found one race this way: the I/O layer's lazily read mmap mode
+could be seen set before the page size it guards (pncx_io.c mmap_mode, now a
+pthread_once).  The writers pass a barrier before their first data call so
+that such first touches are unordered; with the old mmap_mode every case
+here reports it (checked by reverting the fix).  STUB=nodev builds against
+the no-device stub instead (the NC_BYTE / NC_CHAR paths only)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _have_tsan():
+    if shutil.which("gcc") is None:
+        return False
+    lib = subprocess.run(["gcc", "-print-file-name=libtsan.so"], capture_output=True, text=True).stdout.strip()
+    return os.path.isabs(lib) and os.path.exists(lib)
+
+
+@pytest.mark.parametrize("env", [{}, {"PNCX_IO_THREADS": "1", "PNCX_STAGE_MB": "1"}, {"STUB": "nodev"}],
+                         ids=["default", "one-thread-1MiB", "no-device"])
+def test_host_code_tsan_clean(env):
+    if not _have_tsan():
+        pytest.skip("gcc or libtsan not available")
+    e = dict(os.environ, NTHREADS="6", ITERS="2", **env)
+    out = subprocess.run(["bash", os.path.join(ROOT, "tools", "tsan", "run.sh")], capture_output=True,
+                         text=True, env=e, timeout=900)
+    assert out.returncode == 0, (out.stdout[-2000:], out.stderr[-6000:])
+    assert "ThreadSanitizer" not in out.stderr, out.stderr[-6000:]
+    assert "threads ok 6 writers" in out.stdout, out.stdout
