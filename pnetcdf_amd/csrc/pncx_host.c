@@ -140,11 +140,27 @@ int pncx_knob_get(const char *name, long long *value)
     return NC_NOERR;
 }
 
+static int g_nontemporal;
+static size_t g_chunk_bytes, g_pin_min;
+
+/* The environment, read once at load, before any thread of the library
+ * runs (no lazily set globals that two threads could race on): phases,
+ * the A/B knobs and the size settings below. */
 __attribute__((constructor)) static void ph_init(void)
 {
-    const char *e = getenv("PNCX_PHASES");
+    const char *e;
     char nm[64];
     int i;
+    long v;
+    e = getenv("PNCX_NONTEMPORAL");              /* -1: plain accesses (A/B) */
+    g_nontemporal = e ? atoi(e) : 1;
+    e = getenv("PNCX_CHUNK_MB");
+    v = e ? atol(e) : 16;
+    g_chunk_bytes = (size_t)(v > 0 ? v : 16) << 20;
+    e = getenv("PNCX_PIN_MIN_KB");
+    v = e ? atol(e) : 1024;
+    g_pin_min = (size_t)(v > 0 ? v : 1024) << 10;
+    e = getenv("PNCX_PHASES");
     pncx_ph_on = e != NULL ? (atoi(e) < 0 ? 0 : atoi(e) > 2 ? 2 : atoi(e)) : 0;
     for (i = 0; i < PNCXK_NKNOB; i++) {
         snprintf(nm, sizeof nm, "PNCX_%s", g_knob_names[i]);
@@ -283,15 +299,7 @@ static int classify(int dir, int cdf_ver, int xtype, int itype, const void *fill
 
 /* nontemporal ("streaming") loads/stores: on by default (every byte is
  * touched once); PNCX_NONTEMPORAL=-1 selects plain accesses for A/B runs. */
-static int nontemporal_mode(void)
-{
-    static int v = 2;
-    if (v == 2) {
-        const char *e = getenv("PNCX_NONTEMPORAL");
-        v = e ? atoi(e) : 1;
-    }
-    return v;
-}
+static int nontemporal_mode(void) { return g_nontemporal; }
 
 static int launch_op(const op_t *op, const void *src, void *dst, long long n, int *dstatus,
                      void *stream)
@@ -445,17 +453,7 @@ typedef struct ctx_t {
 static ctx_t g_ctx[MAX_DEV];
 static pthread_mutex_t g_ctx_lock = PTHREAD_MUTEX_INITIALIZER;
 
-static size_t chunk_bytes(void)
-{
-    static size_t v = 0;
-    if (v == 0) {
-        const char *e = getenv("PNCX_CHUNK_MB");
-        long mb = e ? atol(e) : 16;
-        if (mb <= 0) mb = 16;
-        v = (size_t)mb << 20;
-    }
-    return v;
-}
+static size_t chunk_bytes(void) { return g_chunk_bytes; }
 
 static ctx_t *get_ctx(void)
 {
@@ -525,17 +523,7 @@ static int ensure_scratch(ctx_t *c, size_t need)
  */
 /* smallest host buffer pinned for a call (PNCX_PIN_MIN_KB, default 1 MiB:
  * the file-level sweep of 256 KiB / 1 MiB / 64 MiB, profiles/r01_file_bench_pin*.json) */
-size_t pncxrt_pin_threshold(void)
-{
-    static size_t v = 0;
-    if (v == 0) {
-        const char *e = getenv("PNCX_PIN_MIN_KB");
-        long kb = e ? atol(e) : 1024;
-        if (kb <= 0) kb = 1024;
-        v = (size_t)kb << 10;
-    }
-    return v;
-}
+size_t pncxrt_pin_threshold(void) { return g_pin_min; }
 
 typedef struct pinned_t { void *p[2]; int n; } pinned_t;
 

@@ -21,23 +21,26 @@ static int g_cu_count[64];
 static int cu_count() {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (g_cu_count[dev] == 0) {
-        int cus = 0;
+    // set by whichever thread asks first; every thread computes the same value
+    int cus = __atomic_load_n(&g_cu_count[dev], __ATOMIC_RELAXED);
+    if (cus == 0) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
             cus <= 0)
             cus = 256;
-        g_cu_count[dev] = cus;
+        __atomic_store_n(&g_cu_count[dev], cus, __ATOMIC_RELAXED);
     }
-    return g_cu_count[dev];
+    return cus;
 }
 
 static int blocks_per_cu() {
     static int v = -1;
-    if (v < 0) {
+    int b = __atomic_load_n(&v, __ATOMIC_RELAXED);
+    if (b < 0) {
         const char *e = getenv("PNCX_BLOCKS_PER_CU");
-        v = (e && atoi(e) > 0) ? atoi(e) : 8;
+        b = (e && atoi(e) > 0) ? atoi(e) : 8;
+        __atomic_store_n(&v, b, __ATOMIC_RELAXED);
     }
-    return v;
+    return b;
 }
 
 namespace pncx {
