@@ -44,19 +44,23 @@ def test_host_code_tsan_clean(env):
     assert "threads ok 6 writers" in out.stdout, out.stdout
 
 
-@pytest.mark.parametrize("dev", ["0", "1"], ids=["host", "device-buffers"])
-def test_api_stack_tsan_clean(dev):
+@pytest.mark.parametrize("san,dev", [("thread", "0"), ("thread", "1"), ("address", "1")],
+                         ids=["tsan-host", "tsan-device-buffers", "asan-ubsan-device-buffers"])
+def test_api_stack_sanitizers_clean(san, dev):
     """The whole host stack behind ncmpi_* (dispatcher, driver, ncmpii, file
     layer, I/O pool) under ThreadSanitizer: api_check's tst_pthread
     restatement (6 threads, the reference's 4 x 5 and 1 MiB records,
     collective and independent) and its 16-thread file-table churn, one MPI
-    process with MPI_THREAD_MULTIPLE (tools/tsan/run_api.sh).  With the
-    dispatcher's mutex removed, the churn reports a race (checked by hand)."""
+    process with MPI_THREAD_MULTIPLE (tools/tsan/run_api.sh); then the
+    single-threaded programs for configs 1, 4 and 5, the put_vara benchmark,
+    define mode and the dispatcher's error returns.  With the dispatcher's
+    mutex removed, the churn reports a race (checked by hand).  SAN=address
+    runs the same programs under AddressSanitizer + UBSan."""
     mpi = os.environ.get("MPI_HOME", "/opt/conda")
     if not _have_tsan() or not os.path.exists(os.path.join(mpi, "lib", "libmpi.so")):
         pytest.skip("gcc/libtsan or MPI not available")
     out = subprocess.run(["bash", os.path.join(ROOT, "tools", "tsan", "run_api.sh"), dev], capture_output=True,
-                         text=True, timeout=900)
+                         text=True, timeout=900, env=dict(os.environ, SAN=san))
     assert out.returncode == 0, (out.stdout[-2000:], out.stderr[-6000:])
-    assert "ThreadSanitizer" not in out.stderr, out.stderr[-6000:]
-    assert f"api tsan ok dev={dev}" in out.stdout, out.stdout[-2000:]
+    assert "Sanitizer" not in out.stderr and "runtime error" not in out.stderr, out.stderr[-6000:]
+    assert f"api {san} ok dev={dev}" in out.stdout, out.stdout[-2000:]
