@@ -2294,6 +2294,7 @@ static int dev_batch(const pncx_seg *segs, int nseg, int *status_out, int *dstat
     int *hstat, i, err = 0, first = NC_NOERR, sval, nclassified = 0, unbatched = 0, swaponly = 1;
     const int async = dstatus != NULL;
     if (nseg <= 0) return NC_NOERR;
+    if (segs == NULL) return NC_EINVAL;
     if (!have_device()) return PNCX_EDEVICE;
     c = get_ctx();
     if (c == NULL) return PNCX_EDEVICE;
@@ -2512,6 +2513,7 @@ int pncx_batch(const pncx_seg *segs, int nseg, int *status_out)
     int i, err = 0, ret;
     uint8_t *arena = NULL;
     if (nseg <= 0) return NC_NOERR;
+    if (segs == NULL) return NC_EINVAL;
     if (!have_device()) return PNCX_EDEVICE;
     c = get_ctx();
     if (c == NULL) return PNCX_EDEVICE;
