@@ -138,6 +138,11 @@ def test_no_cpu_fallback_without_gpu(built):
     L.pncx_preload_pending.restype = ctypes.c_uint
     assert L.pncx_preload_pending(0, mask) == (1 << T.NC_INT) | (1 << T.NC_DOUBLE)
     assert L.pncx_preload_pending(-1, mask) == 0
+    # batches: a missing segment array is an argument error, also without a device
+    st = (ctypes.c_int * 3)()
+    assert L.pncx_dev_batch(None, 3, st, None) == T.NC_EINVAL
+    assert L.pncx_batch(None, 3, st) == T.NC_EINVAL
+    assert L.pncx_dev_batch(None, 0, st, None) == T.NC_NOERR
 
 
 def test_ncmpii_in_swapn_aborts_without_gpu(built):
