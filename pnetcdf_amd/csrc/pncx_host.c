@@ -719,11 +719,25 @@ static long long stage_chunk_elems(const op_t *op, long long n)
  * 25 (copy in / copy out streams); file_bench's big get 32.6 against 22.8
  * GiB/s, C3 22.3 against 16.4, C4 16.3 against 12.0
  * (profiles/r04q_host_modes.txt) */
+/*
+ * Round 6: SDMA copies are the default.  The file-layer fuzz
+ * (tests/test_gpu_file_fuzz.py) and tools/window_probe.py found files and
+ * user buffers holding stale 64-byte pieces after host-buffer puts and gets
+ * whose kernels loaded from or stored to the user's buffer directly (zero
+ * copy through the registration made for the call): 9-10 of 150 probe
+ * rounds with STAGE_ZC, gets still wrong with STAGE_ZCOUT (the kernel
+ * storing into the user buffer), none with STAGE_COPY, where only the copy
+ * engines touch the user's pages (profiles/r06u_window_probe.txt).  Direct
+ * probes of kernel loads and stores on pinned and registered memory
+ * (tools/coherence_probe.hip, tools/visibility_probe.hip,
+ * tools/thp_register_probe.py) did not reproduce it, so the cause is not
+ * pinned down; the zero-copy modes stay for A/B (PNCX_HOST_ZC=1/2).
+ */
 static int stage_mode(long long bytes)
 {
     const long long m = pncx_knob(PNCXK_KNOB_HOST_ZC), mx = pncx_knob(PNCXK_KNOB_HOST_ZC_MAX_MB);
     if (m >= 0) return m > STAGE_ALT ? STAGE_COPY : (int)m;
-    return mx < 0 || bytes <= mx * (1LL << 20) ? STAGE_ZC : STAGE_ALT;
+    return mx < 0 || bytes <= mx * (1LL << 20) ? STAGE_COPY : STAGE_ALT;
 }
 
 static int stage_open(pncx_stage **hp, const op_t *op, int preserve, long long max_chunk, long long total)

@@ -177,7 +177,7 @@ enum {
                                  * stores, 2 zero-copy both ways, 3 copies on
                                  * alternating streams; unset: by size       */
     PNCXK_KNOB_IO_INLINE_MB,    /* requests below: I/O on the calling thread */
-    PNCXK_KNOB_FILE_WINDOW,     /* tmpfs file windows: 0 off, 2 at first use */
+    PNCXK_KNOB_FILE_WINDOW,     /* tmpfs file windows: unset/0 off, 1 at the second touch, 2 at first use */
     PNCXK_KNOB_IO_POPULATE,     /* 0: mapped writes fault their pages in     */
     PNCXK_KNOB_HOST_ZC_MAX_MB,  /* largest call given zero-copy chunks       */
     PNCXK_KNOB_TGAP,            /* 0: 8-bit gap maps stay on k_imap          */
