@@ -649,6 +649,9 @@ static int stage_slots(ctx_t *c, size_t slot_bytes)
  * lazy: loading every kernel file up front made create..enddef 330-530 ms
  * (profiles/r05l_first_call_all_code_objects.txt), and a process converts
  * few external types. */
+/* device slots made at warm-up: a 4 MiB record in 1 MiB chunks needs 2-3
+ * MiB a slot (C1, C3's reads); larger chunks regrow them at first use */
+#define WARM_SLOT_BYTES (16u << 20)
 int pncx_warmup(void)
 {
     ctx_t *c;
@@ -656,6 +659,34 @@ int pncx_warmup(void)
     if (!have_device() || (c = get_ctx()) == NULL) return PNCX_EDEVICE;
     pthread_mutex_lock(&c->lock);
     err = stage_slots(c, 0);
+    /* Since the staging moves host buffers with the copy engines (round 6,
+     * stage_mode), a process's first staged call also paid for the slots'
+     * hipMalloc and the first copy on each stream: the first 4 MiB put of
+     * the C1 pattern took 18 ms against 1.3 with zero copy
+     * (profiles/r06v_c1_first_put.txt).  Both are done here, at enddef. */
+    if (!err) err = stage_slots(c, WARM_SLOT_BYTES);
+    if (!err) err = pncxrt_memcpy_h2d(c->sdbuf[0], c->hstat, 64, c->stream[0]);
+    if (!err) err = pncxrt_memcpy_d2h(c->hstat, c->sdbuf[1], 64, c->stream[1]);
+    if (!err) {
+        /* and copies from and to memory registered for a call, as the user's
+         * buffers are (the first such copy cost ~16 ms more than one from
+         * pinned memory) */
+        const size_t wb = 1u << 20;
+        void *w = aligned_alloc(4096, wb);
+        if (w != NULL) {
+            memset(w, 0, wb);
+            if (pncxrt_host_register(w, wb) == 0) {
+                err = pncxrt_memcpy_h2d(c->sdbuf[0], w, wb, c->stream[0]);
+                if (!err) err = pncxrt_memcpy_d2h(w, c->sdbuf[1], wb, c->stream[1]);
+                if (!err) err = pncxrt_stream_sync(c->stream[0]);
+                if (!err) err = pncxrt_stream_sync(c->stream[1]);
+                pncxrt_host_unregister(w);
+            }
+            free(w);
+        }
+    }
+    if (!err) err = pncxrt_stream_sync(c->stream[0]);
+    if (!err) err = pncxrt_stream_sync(c->stream[1]);
     pthread_mutex_unlock(&c->lock);
     if (!err && pncxrt_load_swap_code() != 0) err = PNCX_EDEVICE;
     return err;

@@ -12,7 +12,9 @@ size and at offsets that move it against 16-byte alignment, through the
 device launch, the device batch, the host-buffer call and the host batch;
 the guards must come back intact and the values must equal the oracle's.
 Host buffers are registered whole, guards included, so that such a store is
-reported here rather than faulting the device.""" 
+reported here rather than faulting the device (the host paths move them
+with the copy engines by default since round 6; PNCX_HOST_ZC=2 runs the
+zero-copy kernels over them)."""
 import ctypes
 
 import numpy as np
