@@ -31,8 +31,7 @@ def _have_tsan():
     return os.path.isabs(lib) and os.path.exists(lib)
 
 
-@pytest.mark.parametrize("env", [{}, {"PNCX_IO_THREADS": "1", "PNCX_STAGE_MB": "1"}, {"STUB": "nodev"}],
-                         ids=["default", "one-thread-1MiB", "no-device"])
+@pytest.mark.parametrize("env", [{"PNCX_STAGE_MB": "1"}, {"STUB": "nodev"}], ids=["1MiB-staging", "no-device"])
 def test_host_code_tsan_clean(env):
     if not _have_tsan():
         pytest.skip("gcc or libtsan not available")
@@ -44,8 +43,8 @@ def test_host_code_tsan_clean(env):
     assert "threads ok 6 writers" in out.stdout, out.stdout
 
 
-@pytest.mark.parametrize("san,dev", [("thread", "0"), ("thread", "1"), ("address", "1")],
-                         ids=["tsan-host", "tsan-device-buffers", "asan-ubsan-device-buffers"])
+@pytest.mark.parametrize("san,dev", [("thread", "1"), ("address", "1")],
+                         ids=["tsan-device-buffers", "asan-ubsan-device-buffers"])
 def test_api_stack_sanitizers_clean(san, dev):
     """The whole host stack behind ncmpi_* (dispatcher, driver, ncmpii, file
     layer, I/O pool) under ThreadSanitizer: api_check's tst_pthread
